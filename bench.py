@@ -1,0 +1,184 @@
+"""Benchmark: Mpixel-samples/s of the MI355X render path on BASELINE.json's single-GPU config.
+
+Workload (configs[1]): synthetic 1024-sphere grid + checker plane, point light, 1920x1080, AA=1
+(scenes/c2_s1024.yaml).  One step = one frame rendered to the AA-averaged f64 image in HBM
+(Camera::render + canvas.rs box average, before `as u8`).  With N ranks (torchrun, one process per
+GPU, RCCL) the frame's rows are split in interleaved 8-row blocks and the tiles are gathered to
+rank 0 with one RCCL gather per step ("scaling": "strong": the frame is fixed).
+
+Also reported: the dominant kernel's roofline (HIP events on the render stream over the timed
+region), and the CPU oracle (test-infrastructure restatement of the reference) timed on a bounded
+row sample on the host cores, whose rows are also compared with the GPU frame (max |d|).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mpixel-samples/s (W×H×AA²) at 1/2/4/8 GPUs; max |Δchannel| vs CPU ref"
+WORKLOADS = {  # name: (scene, W, H, aa, max_depth)
+    "c2_s1024": ("c2_s1024.yaml", 1920, 1080, 1, 5),
+    "c3_s1024_reflect": ("c3_s1024_reflect.yaml", 3840, 2160, 3, 5),
+    "c4_teapot": ("c4_teapot.yaml", 1920, 1080, 2, 5),
+    "c5_area_light": ("c5_area_light.yaml", 1920, 1080, 2, 5),
+    "c1_readme": ("c1_readme.yaml", 800, 600, 1, 5),
+}
+# SURVEY.md §8(d) algorithmic flop model (FMA = 2, sqrt/div = 1): per leaf test and per shade event
+FLOPS = {"sphere": 57, "plane": 13, "tri": 45, "group": 45, "shade": 250}
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP64 MFMA dense) peak, MI355X_MICROARCH.md / SURVEY §8d
+
+
+def scene_counts(desc):
+    kinds = [desc.kind[i] for i in range(desc.n_objects)]
+    top = [desc.top[i] for i in range(desc.n_top)]
+    return {"sphere": sum(1 for i in top if kinds[i] == 0), "plane": sum(1 for i in top if kinds[i] == 1),
+            "group": sum(1 for i in top if kinds[i] == 2), "tri": sum(1 for k in kinds if k in (3, 4)),
+            "objects": len(kinds)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="c2_s1024", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-stride", type=int, default=4, help="CPU sample: one 8-row band in every STRIDE bands")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import rray_amd as R
+
+    scene_file, W, H, aa, depth = WORKLOADS[args.workload]
+    text = open(os.path.join(ROOT, "scenes", scene_file)).read()
+    scene = R.YamlScene(text, W, H, aa, obj_root=os.path.join(ROOT, "scenes"))
+    counts = scene_counts(scene.desc())
+    rend = R.Renderer(local)
+    rend.upload(scene)
+    cam = scene.camera
+    block = 8
+    rows = R.part_rows(H, rank, world, block)
+    max_rows = max(len(R.part_rows(H, p, world, block)) for p in range(world))
+    dev = torch.device("cuda", local)
+    tile = torch.zeros((max_rows, W, 3), dtype=torch.float64, device=dev)
+    gather = [torch.empty_like(tile) for _ in range(world)] if (world > 1 and rank == 0) else None
+    opts = R._lib.RenderOpts(aa, depth, 0, 0, rank, world, block, R._lib.RR_OUT_AVG)
+
+    def step():
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        rend.render_device(cam, opts, None, tile.data_ptr(), stream)
+        if world > 1:
+            dist.gather(tile, gather_list=gather, dst=0)
+
+    def sync():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    sync()
+    rend.kernel_profile(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync()
+    t1 = time.perf_counter()
+    ktimes = rend.kernel_times()
+    rend.kernel_profile(False)
+    stats = rend.last_stats()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    samples_per_frame = W * H * aa * aa
+    value = samples_per_frame * args.steps / elapsed / 1e6
+
+    # roofline of the dominant kernel (rank 0's measurements)
+    dom = max(ktimes, key=lambda k: ktimes[k][0])
+    dom_ms, dom_n = ktimes[dom]
+    per_ray = (FLOPS["sphere"] * counts["sphere"] + FLOPS["plane"] * counts["plane"] + FLOPS["group"] * counts["group"])
+    if dom == "trace":
+        units = stats["rays"]  # closest-hit rays of one frame = launches' rays (full scan, no early exit)
+        flops = units * per_ray + (FLOPS["tri"] * stats["prim_tests"] if counts["tri"] else 0)
+    elif dom == "shadow":
+        units = stats["shadow_rays"]
+        flops = units * per_ray
+    else:
+        units = stats["shade_events"]
+        flops = units * FLOPS["shade"]
+    launches_per_frame = dom_n / args.steps
+    achieved = flops / launches_per_frame / (dom_ms / dom_n / 1e3) / 1e12 if dom_ms > 0 else 0.0
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": traffic, "kernel": dom,
+                "kernel_ms": round(dom_ms / dom_n, 4), "launches_per_step": launches_per_frame,
+                "flops_per_launch": flops / launches_per_frame,
+                "note": "FP64 VALU-bound; peak = MI355X FP64 vector = FP64 MFMA dense 78.6 TF; bit-parity forbids "
+                        "FMA contraction so at most half of it is reachable (DESIGN.md §4)"}
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle
+        from oracle.scene_yaml import build_from_yaml
+
+        threads = min(16, os.cpu_count() or 1)
+        o, ocam = build_from_yaml(text, W, H, aa, obj_root=os.path.join(ROOT, "scenes"))
+        tc = time.perf_counter()
+        canvas, _ = o.render(ocam, max_depth=depth, threads=threads, band=block * aa, band_stride=args.cpu_stride)
+        dt = time.perf_counter() - tc
+        sel = np.array([y for y in range(H * aa) if (y // (block * aa)) % args.cpu_stride == 0])
+        cpu_samples = len(sel) * W * aa
+        cpu = {"value": round(cpu_samples / dt / 1e6, 5), "unit": "Mpixel-samples/s", "cores": threads, "kind": "port",
+               "sample": f"oracle (C++ restatement, reference structure: per-object inverse, full xs list + stable "
+                         f"sort, recursion) on {len(sel) // aa} of {H} output rows (one {block}-row band in every "
+                         f"{args.cpu_stride}), {cpu_samples} samples, {dt:.1f}s"}
+        avg = o.aa_average(np.nan_to_num(canvas), aa)
+        out_rows = sorted(set(int(y) // aa for y in sel))
+        gpu_img = tile[: len(rows)].cpu().numpy()
+        parity = {"rows_checked": len(out_rows),
+                  "max_abs_diff": float(np.max(np.abs(gpu_img[out_rows] - avg[out_rows]))),
+                  "bit_exact_frac": float(np.mean(gpu_img[out_rows] == avg[out_rows]))}
+
+    if rank == 0:
+        line = {"metric": METRIC, "value": round(value, 3), "unit": "Mpixel-samples/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+                "data": "synthetic (scenes/make_scenes.py, seeded)",
+                "config": {"workload": args.workload, "scene": scene_file, "width": W, "height": H, "aa": aa,
+                           "max_depth": depth, "samples_per_step": samples_per_frame, "objects": counts["objects"],
+                           "parallelism": f"row-tiles x{world}" + (" + rccl gather" if world > 1 else "")},
+                "roofline": roofline, "cpu_baseline": cpu, "parity_sample": parity,
+                "kernels_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in ktimes.items() if v[1]},
+                "stats_last_step": {k: stats[k] for k in ("rays", "shadow_rays", "shade_events", "n1n2_scans")}}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    rend.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,188 @@
+/*
+ * rray.h — C ABI of the MI355X (gfx950) render path for davelpz/rray.
+ *
+ * Drop-in boundary for the reference's per-pixel render loop:
+ *   Camera::render(&self, &Scene) -> Canvas        src/raytracer/camera.rs:107-121
+ *     -> Scene::color_at / intersect / shade_hit / is_shadowed / reflected_color /
+ *        refracted_color                           src/raytracer/scene.rs:97-336
+ *     -> Object::intersect (+ local_intersect)     src/raytracer/object.rs:45-48
+ * and its YAML/CLI front-end
+ *   render_scene_from_file(path, w, h, png, aa)    src/raytracer/scene_builder_yaml.rs:429-436
+ *
+ * Everything is extern "C" with plain pointers and sizes so a Rust host binds it with
+ * an `extern "C"` block.  Return codes: 0 = OK, < 0 = error
+ * (the reference's panics, scene_builder_yaml.rs / db.rs, become codes); the message is
+ * available from rr_last_error().  Never aborts or throws across the ABI.
+ *
+ * There is no CPU fallback: every render entry point runs the HIP kernels and fails with
+ * RR_E_HIP when no gfx950 device is usable.
+ */
+#ifndef RRAY_RRAY_H
+#define RRAY_RRAY_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RR_ABI_VERSION 1
+
+/* error codes */
+#define RR_OK 0
+#define RR_E_ARG (-1)        /* invalid argument / inconsistent descriptor */
+#define RR_E_HIP (-2)        /* HIP runtime error (no device, launch failure, ...) */
+#define RR_E_SCENE (-3)      /* scene the reference would panic on (scene_builder_yaml.rs) */
+#define RR_E_NONAFFINE (-4)  /* inverse transform with row 3 != (0,0,0,1) */
+#define RR_E_LIMIT (-5)      /* exceeds a compiled limit (depth, pattern nesting) */
+#define RR_E_IO (-6)         /* file missing / unreadable / unwritable */
+#define RR_E_NAN (-7)        /* NaN intersection t: reference panics in sort (scene.rs:104) */
+
+/* object kinds — Sphere, Plane, Group, Triangle, SmoothTriangle (src/raytracer/object/) */
+enum { RR_SPHERE = 0, RR_PLANE = 1, RR_GROUP = 2, RR_TRIANGLE = 3, RR_SMOOTH_TRIANGLE = 4 };
+/* pattern kinds — PatternType (src/raytracer/material/pattern.rs:10-21), in-scope subset */
+enum { RR_PAT_TEST = 0, RR_PAT_SOLID = 1, RR_PAT_STRIPE = 2, RR_PAT_GRADIENT = 3,
+       RR_PAT_RING = 4, RR_PAT_CHECKER = 5, RR_PAT_BLEND = 6 };
+/* light kinds — LightType (src/raytracer/light.rs:10-14) */
+enum { RR_LIGHT_POINT = 0, RR_LIGHT_AREA = 1 };
+
+#define RR_MAX_DEPTH 8          /* max `remaining` (render uses 5, camera.rs:113) */
+#define RR_MAX_GROUP_DEPTH 6    /* nested group levels */
+#define RR_MAX_PATTERN_DEPTH 8  /* nested pattern levels */
+
+/*
+ * The scene exactly as the reference's object registry holds it (object/db.rs:11-13 +
+ * Scene{light, ids}, scene.rs:24-27).  All arrays are caller-owned and copied by
+ * rr_scene_upload.  Object ids index every per-object array.
+ */
+typedef struct {
+    int32_t n_objects;
+    const int32_t* kind;         /* RR_SPHERE.. per object */
+    const int32_t* parent;       /* parent group id or -1 (Object::get_parent_id) */
+    const double* transform;     /* n_objects x 16, row-major (Matrix.data, matrix.rs:20-25) */
+    const double* inverse;       /* optional n_objects x 16; NULL: computed like matrix.rs:389-412 */
+    const int32_t* material;     /* material index per object (ignored for groups) */
+    const double* tri;           /* n_objects x 18: p1,p2,p3,n1,n2,n3 (triangles; NULL if none) */
+    const int32_t* child_start;  /* per object: offset into children[] (groups) */
+    const int32_t* child_count;  /* per object: number of children (Group.child_ids order) */
+    const int32_t* children;
+    int32_t n_top;               /* Scene.ids (tie-break order of the stable sort) */
+    const int32_t* top;
+
+    int32_t n_materials;         /* Material (material.rs:35-44) */
+    const double* mat;           /* n_materials x 7: ambient, diffuse, specular, shininess,
+                                    reflective, transparency, refractive_index */
+    const int32_t* mat_pattern;  /* root pattern per material */
+
+    int32_t n_patterns;          /* Pattern tree nodes (pattern.rs:23-27) */
+    const int32_t* pat_kind;
+    const int32_t* pat_a;        /* child pattern ids (-1 if none) */
+    const int32_t* pat_b;
+    const double* pat_color;     /* n_patterns x 3 (Solid) */
+    const double* pat_scale;     /* n_patterns (Blend) */
+    const double* pat_transform; /* n_patterns x 16 */
+
+    int32_t n_lights;            /* Light (light.rs:17-21) */
+    const int32_t* light_kind;
+    const double* light;         /* n_lights x 15: position, intensity, corner, u, v */
+    const int32_t* light_level;  /* area light sample level (light.rs:13) */
+} rr_scene_desc;
+
+/* Camera (camera.rs:18-27): hsize/vsize are the SUPERSAMPLED sizes (W*aa, H*aa). */
+typedef struct {
+    int64_t hsize, vsize;
+    double field_of_view, pixel_size, half_width, half_height;
+    double transform[16];
+} rr_camera;
+
+/* render options */
+typedef struct {
+    int32_t aa;            /* anti-aliasing level; camera sizes are W*aa x H*aa */
+    int32_t max_depth;     /* reflect/refract recursion budget (5 in camera.rs:113) */
+    uint64_t seed;         /* area-light jitter seed (replaces thread_rng, light.rs:57-59) */
+    int32_t jitter_mode;   /* 0 = counter hash jitter, 1 = cell centre */
+    int32_t part, nparts;  /* row sharding: output rows y with (y/block_rows)%nparts == part */
+    int32_t block_rows;    /* rows per interleaved block (default 8) */
+    int32_t flags;         /* RR_OUT_* */
+} rr_render_opts;
+#define RR_OUT_CANVAS 1    /* write the supersampled canvas (Canvas.pixels layout) */
+#define RR_OUT_AVG 2       /* write the AA-averaged image (canvas.rs:76-96, before `as u8`) */
+
+typedef struct {
+    uint64_t rays;          /* closest-hit rays (primary + reflected + refracted) */
+    uint64_t shadow_rays;   /* is_shadowed rays */
+    uint64_t shade_events;  /* shade_hit calls */
+    uint64_t n1n2_scans;    /* prepare_computations container walks (transparent hits) */
+    uint64_t group_tests, group_hits;
+    uint64_t samples;       /* pixel x AA samples rendered */
+    uint64_t prim_tests;    /* reference-equivalent leaf tests */
+    double kernel_ms;       /* render + AA kernels, HIP events */
+} rr_stats;
+
+typedef struct rr_ctx rr_ctx;
+typedef struct rr_scene rr_scene;
+
+/* ---- library ---- */
+int32_t rr_abi_version(void);
+const char* rr_last_error(void);            /* thread-local message of the last failure */
+int rr_device_count(int* out);
+
+/* ---- context: one device, one stream (not thread-safe; one render at a time) ---- */
+int rr_create(int device, rr_ctx** out);
+void rr_destroy(rr_ctx* ctx);
+/* flattens (DFS order, 3x4 inverses, group AABBs) and uploads to HBM (scene.rs, group.rs) */
+int rr_scene_upload(rr_ctx* ctx, const rr_scene_desc* desc);
+
+/* Camera::new (camera.rs:41-63) */
+int rr_camera_new(int64_t hsize, int64_t vsize, double field_of_view, const double transform[16], rr_camera* out);
+
+/* Camera::render (camera.rs:107-121).  Host buffers:
+ *   out_canvas: hsize*vsize_part*3 doubles (RR_OUT_CANVAS) — identical layout to Canvas.pixels;
+ *   out_avg:    W*rows_part*3 doubles (RR_OUT_AVG).
+ * Rows are this part's rows in increasing order (see rr_part_rows).  Blocking. */
+int rr_render(rr_ctx* ctx, const rr_camera* cam, const rr_render_opts* opts, double* out_canvas, double* out_avg,
+              rr_stats* stats);
+/* Same, into DEVICE buffers on the context's device, enqueued on `hip_stream` (NULL: ctx stream)
+ * and NOT synchronised — for collectives that consume the tile straight from HBM. */
+int rr_render_device(rr_ctx* ctx, const rr_camera* cam, const rr_render_opts* opts, void* d_canvas, void* d_avg,
+                     void* hip_stream);
+/* AA-averaged rows owned by `part` of `nparts` (interleaved blocks of block_rows output rows). */
+int64_t rr_part_rows(int64_t height, int32_t part, int32_t nparts, int32_t block_rows, int64_t* rows_out);
+/* Per-kernel HIP-event timing on the context's stream.  rr_kernel_profile(ctx, 1) resets and enables
+ * it; rr_kernel_times fills accumulated milliseconds and launch counts per kernel in the order
+ * trace, n1n2, shade, shadow, finish, combine, aa (returns the number of kernels, 7). */
+int rr_kernel_profile(rr_ctx* ctx, int enable);
+int rr_kernel_times(rr_ctx* ctx, double* ms, uint64_t* launches, int32_t n);
+/* stats of the last rr_render/rr_render_device on this context (synchronises) */
+int rr_last_stats(rr_ctx* ctx, rr_stats* stats);
+
+/* Scene::color_at (scene.rs:128-136) for a batch of rays (rr_color_at), and
+ * Scene::is_shadowed (scene.rs:234-245) for a batch of point/light pairs.  Host buffers. */
+int rr_color_at(rr_ctx* ctx, int64_t n, const double* origins, const double* directions, int32_t remaining,
+                uint64_t seed, int32_t jitter_mode, double* out_rgb);
+int rr_is_shadowed(rr_ctx* ctx, int64_t n, const double* points, const double* light_positions, int32_t* out);
+
+/* Host-only inspection of the flattening (no device needed): per-object inverse transforms as the
+ * kernels use them (4x4, row 3 == 0,0,0,1), group bounding boxes (group.rs:128-149; zeros for
+ * non-groups) and each object's index in the flattened depth-first order (-1: not in the tree).
+ * Any output pointer may be NULL. */
+int rr_scene_inspect(const rr_scene_desc* desc, double* inverses, double* group_aabbs, int32_t* node_of_object);
+
+/* ---- front-end: scene_builder_yaml.rs / load_obj.rs / canvas.rs / main.rs ---- */
+/* render_scene_from_str up to camera.render: parse YAML (first document), build the scene.
+ * obj_root: directory relative OBJ paths are resolved against (NULL: current directory). */
+int rr_scene_from_yaml(const char* yaml_text, const char* obj_root, int64_t width, int64_t height, int32_t aa,
+                       rr_scene** out_scene, rr_camera* out_camera);
+const rr_scene_desc* rr_scene_desc_of(const rr_scene* scene);
+void rr_scene_free(rr_scene* scene);
+/* canvas.rs:76-105 + write_to_file: AA-averaged f64 image -> RGBA8 (`as u8`) -> PNG */
+int rr_quantize(const double* avg, int64_t n_pixels, uint8_t* rgba);
+int rr_write_png(const char* path, const uint8_t* rgba, int64_t width, int64_t height);
+/* render_scene_from_file (scene_builder_yaml.rs:429-436) on `device` */
+int rr_render_scene_from_file(const char* path, int64_t width, int64_t height, const char* png_file, int32_t aa,
+                              int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RRAY_RRAY_H */

@@ -1,0 +1,110 @@
+"""ctypes binding of librray_amd.so (include/rray/rray.h).
+
+Loading fails loudly when the in-tree library is missing: there is no CPU fallback.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_lib", "librray_amd.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "rray", "rray.h")
+
+RR_OK = 0
+ERRORS = {-1: "RR_E_ARG", -2: "RR_E_HIP", -3: "RR_E_SCENE", -4: "RR_E_NONAFFINE", -5: "RR_E_LIMIT", -6: "RR_E_IO",
+          -7: "RR_E_NAN"}
+RR_OUT_CANVAS, RR_OUT_AVG = 1, 2
+SPHERE, PLANE, GROUP, TRIANGLE, SMOOTH_TRIANGLE = range(5)
+PAT = {"test": 0, "solid": 1, "stripe": 2, "gradient": 3, "ring": 4, "checker": 5, "blend": 6}
+LIGHT_POINT, LIGHT_AREA = 0, 1
+KERNELS = ["trace", "n1n2", "shade", "shadow", "finish", "combine", "aa"]
+
+_D = C.POINTER(C.c_double)
+_I = C.POINTER(C.c_int32)
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [("n_objects", C.c_int32), ("kind", _I), ("parent", _I), ("transform", _D), ("inverse", _D),
+                ("material", _I), ("tri", _D), ("child_start", _I), ("child_count", _I), ("children", _I),
+                ("n_top", C.c_int32), ("top", _I), ("n_materials", C.c_int32), ("mat", _D), ("mat_pattern", _I),
+                ("n_patterns", C.c_int32), ("pat_kind", _I), ("pat_a", _I), ("pat_b", _I), ("pat_color", _D),
+                ("pat_scale", _D), ("pat_transform", _D), ("n_lights", C.c_int32), ("light_kind", _I),
+                ("light", _D), ("light_level", _I)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("hsize", C.c_int64), ("vsize", C.c_int64), ("field_of_view", C.c_double),
+                ("pixel_size", C.c_double), ("half_width", C.c_double), ("half_height", C.c_double),
+                ("transform", C.c_double * 16)]
+
+
+class RenderOpts(C.Structure):
+    _fields_ = [("aa", C.c_int32), ("max_depth", C.c_int32), ("seed", C.c_uint64), ("jitter_mode", C.c_int32),
+                ("part", C.c_int32), ("nparts", C.c_int32), ("block_rows", C.c_int32), ("flags", C.c_int32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("shade_events", C.c_uint64),
+                ("n1n2_scans", C.c_uint64), ("group_tests", C.c_uint64), ("group_hits", C.c_uint64),
+                ("samples", C.c_uint64), ("prim_tests", C.c_uint64), ("kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+EXPORTS = ["rr_abi_version", "rr_last_error", "rr_device_count", "rr_create", "rr_destroy", "rr_scene_upload",
+           "rr_camera_new", "rr_render", "rr_render_device", "rr_part_rows", "rr_kernel_profile", "rr_kernel_times",
+           "rr_last_stats", "rr_color_at",
+           "rr_is_shadowed", "rr_scene_inspect", "rr_scene_from_yaml", "rr_scene_desc_of", "rr_scene_free", "rr_quantize",
+           "rr_write_png", "rr_render_scene_from_file"]
+
+_lib = None
+
+
+class RRError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def lib():
+    """The loaded library; raises when the HIP build is missing (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH)
+    L.rr_abi_version.restype = C.c_int32
+    L.rr_last_error.restype = C.c_char_p
+    L.rr_device_count.argtypes = [C.POINTER(C.c_int)]
+    L.rr_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+    L.rr_destroy.argtypes = [C.c_void_p]
+    L.rr_scene_upload.argtypes = [C.c_void_p, C.POINTER(SceneDesc)]
+    L.rr_camera_new.argtypes = [C.c_int64, C.c_int64, C.c_double, _D, C.POINTER(Camera)]
+    L.rr_render.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(RenderOpts), _D, _D, C.POINTER(Stats)]
+    L.rr_render_device.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(RenderOpts), C.c_void_p, C.c_void_p,
+                                   C.c_void_p]
+    L.rr_part_rows.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int64)]
+    L.rr_part_rows.restype = C.c_int64
+    L.rr_kernel_profile.argtypes = [C.c_void_p, C.c_int]
+    L.rr_kernel_times.argtypes = [C.c_void_p, _D, C.POINTER(C.c_uint64), C.c_int32]
+    L.rr_last_stats.argtypes = [C.c_void_p, C.POINTER(Stats)]
+    L.rr_color_at.argtypes = [C.c_void_p, C.c_int64, _D, _D, C.c_int32, C.c_uint64, C.c_int32, _D]
+    L.rr_is_shadowed.argtypes = [C.c_void_p, C.c_int64, _D, _D, _I]
+    L.rr_scene_inspect.argtypes = [C.POINTER(SceneDesc), _D, _D, _I]
+    L.rr_scene_from_yaml.argtypes = [C.c_char_p, C.c_char_p, C.c_int64, C.c_int64, C.c_int32, C.POINTER(C.c_void_p),
+                                     C.POINTER(Camera)]
+    L.rr_scene_desc_of.argtypes = [C.c_void_p]
+    L.rr_scene_desc_of.restype = C.POINTER(SceneDesc)
+    L.rr_scene_free.argtypes = [C.c_void_p]
+    L.rr_quantize.argtypes = [_D, C.c_int64, C.POINTER(C.c_uint8)]
+    L.rr_write_png.argtypes = [C.c_char_p, C.POINTER(C.c_uint8), C.c_int64, C.c_int64]
+    L.rr_render_scene_from_file.argtypes = [C.c_char_p, C.c_int64, C.c_int64, C.c_char_p, C.c_int32, C.c_int]
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != RR_OK:
+        raise RRError(rc, lib().rr_last_error().decode(errors="replace"))
+    return rc

@@ -1,0 +1,568 @@
+// api.cpp — the C ABI of include/rray/rray.h: device context, scene upload, the wavefront level
+// loop that replaces Camera::render (camera.rs:107-121), and the batch query entry points.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rray/rray.h"
+#include "flatten.hpp"
+#include "kernels.hpp"
+#include "rr_math.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+#define HIPCHK(expr)                                                                            \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return fail(RR_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));          \
+    } while (0)
+
+// grow-only device buffer
+struct DBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        size_t cap = std::max(want, (size_t)256);
+        hipError_t e = hipMalloc(&p, cap);
+        if (e == hipSuccess) bytes = cap;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+};
+
+}  // namespace
+
+void rr_set_error(const char* msg) { g_err = msg ? msg : ""; }
+
+struct rr_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool has_scene = false;
+    rr::HostScene host;
+    rr::DevScene S{};
+    DBuf nodes, groups, tris, mats, pats, lights, sr_light, sr_s;
+    int32_t n_sr = 0;
+    // workspace
+    DBuf counters, lcount, hit, n12, sr, lit, sb, n1n2, ev_a, ev_b, canvas, rays0, qout;
+    std::vector<DBuf> comb;  // one per level
+    unsigned int* h_lcount = nullptr;  // pinned
+    unsigned long long* h_counters = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    rr_stats last{};
+    bool stats_pending = false;
+    int64_t batch = (int64_t)1 << 23;
+    // per-kernel timing (rr_kernel_times)
+    bool profile = false;
+    rr::KernelProf prof;
+    double kms[rr::K_COUNT] = {0};
+    uint64_t kcount[rr::K_COUNT] = {0};
+};
+
+namespace {
+
+template <class T>
+hipError_t upload(DBuf& b, const std::vector<T>& v, hipStream_t st) {
+    hipError_t e = b.ensure(std::max<size_t>(v.size() * sizeof(T), 16));
+    if (e != hipSuccess) return e;
+    if (!v.empty()) e = hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st);
+    return e;
+}
+
+int check_opts(const rr_camera* cam, const rr_render_opts* o) {
+    if (!cam || !o) return fail(RR_E_ARG, "null camera/options");
+    if (o->aa < 1) return fail(RR_E_ARG, "aa must be >= 1");
+    if (o->max_depth < 0 || o->max_depth > RR_MAX_DEPTH) return fail(RR_E_LIMIT, "max_depth out of range");
+    if (o->nparts < 1 || o->part < 0 || o->part >= o->nparts) return fail(RR_E_ARG, "bad part/nparts");
+    if (cam->hsize <= 0 || cam->vsize <= 0 || cam->hsize % o->aa || cam->vsize % o->aa)
+        return fail(RR_E_ARG, "camera size must be a positive multiple of aa");
+    if (cam->hsize > (1ll << 31) || cam->vsize > (1ll << 31)) return fail(RR_E_LIMIT, "camera too large");
+    return RR_OK;
+}
+
+rr::DevCamera dev_camera(const rr_camera* c) {
+    rr::DevCamera d{};
+    d.hsize = c->hsize;
+    d.vsize = c->vsize;
+    d.half_width = c->half_width;
+    d.half_height = c->half_height;
+    d.pixel_size = c->pixel_size;
+    rr::M4 t{};
+    for (int i = 0; i < 16; ++i) t.m[i] = c->transform[i];
+    rr::M4 inv = rr::inverse(t);  // camera.rs:85 (cached inverse, same value)
+    for (int i = 0; i < 16; ++i) d.inv[i] = inv.m[i];
+    return d;
+}
+
+int64_t part_rows_count(int64_t height, int32_t part, int32_t nparts, int32_t block) {
+    int64_t n = 0;
+    for (int64_t b0 = (int64_t)part * block; b0 < height; b0 += (int64_t)nparts * block)
+        n += std::min<int64_t>(block, height - b0);
+    return n;
+}
+
+// Runs the wavefront levels for `total` level-0 events; level-0 rays come from the camera or from
+// ctx->rays0 (color_at).  Results (color_at values) land in `out` (3 doubles per event).
+int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max_depth, double* out) {
+    hipStream_t st = c->stream;
+    const int64_t B = std::max<int64_t>(1, c->batch);
+    for (int64_t base = 0; base < total; base += B) {
+        const int64_t nb = std::min(B, total - base);
+        std::vector<int64_t> level_n;
+        int64_t n = nb;
+        DBuf* cur_ev = nullptr;
+        DBuf* nxt_ev = &c->ev_a;
+        for (int d = 0; d <= max_depth && n > 0; ++d) {
+            if ((int)c->comb.size() <= d) c->comb.resize(d + 1);
+            const int64_t nsr = std::max<int64_t>(c->n_sr, 1);
+            HIPCHK(c->hit.ensure(n * sizeof(rr::HitRec)));
+            HIPCHK(c->n12.ensure(n * 2 * sizeof(double)));
+            HIPCHK(c->sr.ensure(n * sizeof(rr::ShadeRec)));
+            HIPCHK(c->comb[d].ensure(n * sizeof(rr::CombRec)));
+            HIPCHK(c->lit.ensure(n * sizeof(int32_t)));
+            HIPCHK(c->sb.ensure(n * nsr));
+            HIPCHK(c->n1n2.ensure(n * sizeof(int32_t)));
+            const bool children_possible = d < max_depth;
+            if (children_possible) HIPCHK(nxt_ev->ensure(2 * n * sizeof(rr::Event)));
+            HIPCHK(hipMemsetAsync(c->lcount.p, 0, rr::LC_COUNT * sizeof(unsigned int), st));
+            rr::LevelArgs A = base_args;
+            A.base = base;
+            A.level = d;
+            A.rem = max_depth - d;
+            A.n = n;
+            A.ev = cur_ev ? cur_ev->as<rr::Event>() : nullptr;
+            A.hit = c->hit.as<rr::HitRec>();
+            A.n12 = c->n12.as<double>();
+            A.sr = c->sr.as<rr::ShadeRec>();
+            A.comb = c->comb[d].as<rr::CombRec>();
+            A.next = children_possible ? nxt_ev->as<rr::Event>() : nullptr;
+            A.lit = c->lit.as<int32_t>();
+            A.sb = c->sb.as<uint8_t>();
+            A.n1n2_list = c->n1n2.as<int32_t>();
+            A.lcount = c->lcount.as<unsigned int>();
+            A.n_sr = c->n_sr;
+            A.sr_light = c->sr_light.as<int32_t>();
+            A.sr_s = c->sr_s.as<int32_t>();
+            A.counters = c->counters.as<unsigned long long>();
+            HIPCHK(rr::launch_level(c->S, A, n * (int64_t)c->n_sr, st, c->profile ? &c->prof : nullptr));
+            level_n.push_back(n);
+            if (!children_possible) break;
+            HIPCHK(hipMemcpyAsync(c->h_lcount, c->lcount.p, rr::LC_COUNT * sizeof(unsigned int), hipMemcpyDeviceToHost,
+                                  st));
+            HIPCHK(hipStreamSynchronize(st));
+            n = (int64_t)c->h_lcount[rr::LC_CHILDREN];
+            cur_ev = nxt_ev;
+            nxt_ev = (nxt_ev == &c->ev_a) ? &c->ev_b : &c->ev_a;
+        }
+        // bottom-up shade_hit sums (scene.rs:172-177); level 0 writes the results
+        for (int d = (int)level_n.size() - 1; d >= 0; --d) {
+            rr::CombArgs C{};
+            C.level = d;
+            C.n = level_n[d];
+            C.base = base;
+            C.comb = c->comb[d].as<rr::CombRec>();
+            C.parent_comb = d > 0 ? c->comb[d - 1].as<rr::CombRec>() : nullptr;
+            C.out = out;
+            HIPCHK(rr::launch_combine(C, st, c->profile ? &c->prof : nullptr));
+        }
+    }
+    return RR_OK;
+}
+
+void collect_stats(rr_ctx* c, rr_stats* s) {
+    std::memset(s, 0, sizeof(*s));
+    const unsigned long long* h = c->h_counters;
+    s->rays = h[rr::C_RAYS];
+    s->shadow_rays = h[rr::C_SHADOW];
+    s->shade_events = h[rr::C_SHADE];
+    s->n1n2_scans = h[rr::C_N1N2];
+    s->group_tests = h[rr::C_GROUP_TESTS];
+    s->group_hits = h[rr::C_GROUP_HITS];
+    s->samples = h[rr::C_SAMPLES];
+    s->prim_tests = h[rr::C_PRIM_TESTS];
+}
+
+int resolve_prof(rr_ctx* c) {
+    for (auto& m : c->prof.marks) {
+        HIPCHK(hipEventSynchronize(m.second.second));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, m.second.first, m.second.second));
+        c->kms[m.first] += ms;
+        c->kcount[m.first] += 1;
+    }
+    c->prof.marks.clear();
+    c->prof.used = 0;
+    return RR_OK;
+}
+
+int finish_stats(rr_ctx* c) {
+    if (!c->stats_pending) return RR_OK;
+    HIPCHK(hipEventSynchronize(c->e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
+    collect_stats(c, &c->last);
+    c->last.kernel_ms = ms;
+    c->stats_pending = false;
+    return RR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t rr_abi_version(void) { return RR_ABI_VERSION; }
+const char* rr_last_error(void) { return g_err.c_str(); }
+
+int rr_device_count(int* out) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    if (out) *out = n;
+    return e == hipSuccess ? RR_OK : fail(RR_E_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+}
+
+int rr_create(int device, rr_ctx** out) {
+    if (!out) return fail(RR_E_ARG, "null out");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RR_E_HIP, "no HIP device available");
+    if (device < 0 || device >= n) return fail(RR_E_ARG, "device index out of range");
+    HIPCHK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(RR_E_HIP, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950 only");
+    rr_ctx* c = new rr_ctx();
+    c->device = device;
+    if (const char* b = std::getenv("RRAY_BATCH")) c->batch = std::max<int64_t>(1024, std::atoll(b));
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&c->e0);
+    if (e == hipSuccess) e = hipEventCreate(&c->e1);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_lcount, 64 * sizeof(unsigned int), hipHostMallocDefault);
+    if (e == hipSuccess)
+        e = hipHostMalloc((void**)&c->h_counters, rr::C_COUNT * sizeof(unsigned long long), hipHostMallocDefault);
+    if (e == hipSuccess) e = c->counters.ensure(rr::C_COUNT * sizeof(unsigned long long));
+    if (e == hipSuccess) e = c->lcount.ensure(64 * sizeof(unsigned int));
+    if (e != hipSuccess) {
+        rr_destroy(c);
+        return fail(RR_E_HIP, std::string("context setup: ") + hipGetErrorString(e));
+    }
+    *out = c;
+    return RR_OK;
+}
+
+void rr_destroy(rr_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (DBuf* b : {&c->nodes, &c->groups, &c->tris, &c->mats, &c->pats, &c->lights, &c->sr_light, &c->sr_s,
+                    &c->counters, &c->lcount, &c->hit, &c->n12, &c->sr, &c->lit, &c->sb, &c->n1n2, &c->ev_a, &c->ev_b,
+                    &c->canvas, &c->rays0, &c->qout})
+        b->release();
+    for (auto& b : c->comb) b.release();
+    for (hipEvent_t e : c->prof.pool) (void)hipEventDestroy(e);
+    if (c->h_lcount) (void)hipHostFree(c->h_lcount);
+    if (c->h_counters) (void)hipHostFree(c->h_counters);
+    if (c->e0) (void)hipEventDestroy(c->e0);
+    if (c->e1) (void)hipEventDestroy(c->e1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
+    if (!c || !d) return fail(RR_E_ARG, "null context/descriptor");
+    std::string err;
+    rr::HostScene hs;
+    int rc = rr::flatten_scene(*d, hs, err);
+    if (rc != RR_OK) return fail(rc, err);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    HIPCHK(upload(c->nodes, hs.nodes, st));
+    HIPCHK(upload(c->groups, hs.groups, st));
+    HIPCHK(upload(c->tris, hs.tris, st));
+    HIPCHK(upload(c->mats, hs.mats, st));
+    HIPCHK(upload(c->pats, hs.pats, st));
+    HIPCHK(upload(c->lights, hs.lights, st));
+    // shadow slots: one per point light, level^2 per area light (scene.rs:181-214)
+    std::vector<int32_t> sl, ss;
+    for (size_t li = 0; li < hs.lights.size(); ++li) {
+        const rr::DevLight& L = hs.lights[li];
+        int amount = L.kind == RR_LIGHT_POINT ? 1 : L.level * L.level;
+        for (int s = 0; s < amount; ++s) {
+            sl.push_back((int32_t)li);
+            ss.push_back(s);
+        }
+    }
+    HIPCHK(upload(c->sr_light, sl, st));
+    HIPCHK(upload(c->sr_s, ss, st));
+    HIPCHK(hipStreamSynchronize(st));
+    c->n_sr = (int32_t)sl.size();
+    c->host = std::move(hs);
+    rr::DevScene& S = c->S;
+    S.nodes = c->nodes.as<rr::DevNode>();
+    S.groups = c->groups.as<rr::DevGroup>();
+    S.tris = c->tris.as<rr::DevTri>();
+    S.mats = c->mats.as<rr::DevMaterial>();
+    S.pats = c->pats.as<rr::DevPattern>();
+    S.lights = c->lights.as<rr::DevLight>();
+    S.n_nodes = (int32_t)c->host.nodes.size();
+    S.n_lights = (int32_t)c->host.lights.size();
+    S.has_transparent = c->host.has_transparent;
+    S.has_groups = c->host.groups.empty() ? 0 : 1;
+    c->has_scene = true;
+    return RR_OK;
+}
+
+int rr_scene_inspect(const rr_scene_desc* d, double* inverses, double* group_aabbs, int32_t* node_of_object) {
+    if (!d) return fail(RR_E_ARG, "null descriptor");
+    std::string err;
+    rr::HostScene hs;
+    int rc = rr::flatten_scene(*d, hs, err);
+    if (rc != RR_OK) return fail(rc, err);
+    for (int i = 0; i < d->n_objects; ++i) {
+        int node = hs.node_of_object[i];
+        if (node_of_object) node_of_object[i] = node;
+        if (inverses) {
+            double* o = inverses + 16 * (size_t)i;
+            if (node >= 0) {
+                for (int k = 0; k < 12; ++k) o[k] = hs.nodes[node].inv[k];
+            } else {
+                for (int k = 0; k < 12; ++k) o[k] = 0.0;
+            }
+            o[12] = 0.0;
+            o[13] = 0.0;
+            o[14] = 0.0;
+            o[15] = 1.0;
+        }
+        if (group_aabbs) {
+            double* o = group_aabbs + 6 * (size_t)i;
+            for (int k = 0; k < 6; ++k) o[k] = 0.0;
+            if (node >= 0 && hs.nodes[node].kind == RR_GROUP)
+                for (int k = 0; k < 6; ++k) o[k] = hs.groups[hs.nodes[node].aux].aabb[k];
+        }
+    }
+    return RR_OK;
+}
+
+int rr_camera_new(int64_t hsize, int64_t vsize, double fov, const double transform[16], rr_camera* out) {
+    if (!out || hsize <= 0 || vsize <= 0) return fail(RR_E_ARG, "bad camera size");
+    double half_view = std::tan(fov / 2.0);  // camera.rs:41-63
+    double aspect = (double)hsize / (double)vsize;
+    double hw, hh;
+    if (aspect >= 1.0) {
+        hw = half_view;
+        hh = half_view / aspect;
+    } else {
+        hw = half_view * aspect;
+        hh = half_view;
+    }
+    out->hsize = hsize;
+    out->vsize = vsize;
+    out->field_of_view = fov;
+    out->half_width = hw;
+    out->half_height = hh;
+    out->pixel_size = (hw * 2.0) / (double)hsize;
+    rr::M4 id = rr::identity();
+    for (int i = 0; i < 16; ++i) out->transform[i] = transform ? transform[i] : id.m[i];
+    return RR_OK;
+}
+
+int64_t rr_part_rows(int64_t height, int32_t part, int32_t nparts, int32_t block, int64_t* rows_out) {
+    if (nparts < 1 || part < 0 || part >= nparts || block < 1 || height < 0) return fail(RR_E_ARG, "bad partition");
+    int64_t n = 0;
+    for (int64_t b0 = (int64_t)part * block; b0 < height; b0 += (int64_t)nparts * block)
+        for (int64_t y = b0; y < std::min<int64_t>(b0 + block, height); ++y) {
+            if (rows_out) rows_out[n] = y;
+            ++n;
+        }
+    return n;
+}
+
+int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, void* d_canvas, void* d_avg,
+                     void* hip_stream) {
+    if (!c) return fail(RR_E_ARG, "null context");
+    if (!c->has_scene) return fail(RR_E_ARG, "no scene uploaded");
+    int rc = check_opts(cam, o);
+    if (rc != RR_OK) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    const int32_t block = o->block_rows > 0 ? o->block_rows : 8;
+    const int64_t H = cam->vsize / o->aa, W = cam->hsize / o->aa;
+    const int64_t rows = part_rows_count(H, o->part, o->nparts, block);
+    const int64_t local_rows = rows * o->aa;
+    const int64_t total = local_rows * cam->hsize;
+    hipStream_t st = c->stream;
+    hipEvent_t ready = nullptr;
+    if (hip_stream) {  // order after the caller's stream
+        HIPCHK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(ready, (hipStream_t)hip_stream));
+        HIPCHK(hipStreamWaitEvent(st, ready, 0));
+    }
+    double* canvas = static_cast<double*>(d_canvas);
+    if (!canvas) {
+        HIPCHK(c->canvas.ensure(std::max<int64_t>(total, 1) * 3 * sizeof(double)));
+        canvas = c->canvas.as<double>();
+    }
+    HIPCHK(hipMemsetAsync(c->counters.p, 0, rr::C_COUNT * sizeof(unsigned long long), st));
+    HIPCHK(hipEventRecord(c->e0, st));
+    rr::LevelArgs A{};
+    A.cam = dev_camera(cam);
+    A.hs = cam->hsize;
+    A.aa = o->aa;
+    A.part = o->part;
+    A.nparts = o->nparts;
+    A.block_rows = block;
+    A.rays0 = nullptr;
+    A.seed = o->seed;
+    A.jitter_mode = o->jitter_mode;
+    rc = run_levels(c, A, total, o->max_depth, canvas);
+    if (rc != RR_OK) return rc;
+    if (d_avg)
+        HIPCHK(rr::launch_aa(canvas, static_cast<double*>(d_avg), W, rows, o->aa, st,
+                             c->profile ? &c->prof : nullptr));
+    HIPCHK(hipEventRecord(c->e1, st));
+    HIPCHK(hipMemcpyAsync(c->h_counters, c->counters.p, rr::C_COUNT * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, st));
+    if (hip_stream) {  // the caller's stream waits for the tile
+        HIPCHK(hipEventRecord(ready, st));
+        HIPCHK(hipStreamWaitEvent((hipStream_t)hip_stream, ready, 0));
+        HIPCHK(hipEventDestroy(ready));
+    }
+    c->stats_pending = true;
+    // C_SAMPLES is not incremented by the wavefront kernels; it is the level-0 event count
+    c->h_counters[rr::C_SAMPLES] = 0;
+    c->last.samples = (uint64_t)total;
+    return RR_OK;
+}
+
+int rr_kernel_profile(rr_ctx* c, int enable) {
+    if (!c) return fail(RR_E_ARG, "null context");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    int rc = resolve_prof(c);
+    if (rc != RR_OK) return rc;
+    c->profile = enable != 0;
+    for (int k = 0; k < rr::K_COUNT; ++k) {
+        c->kms[k] = 0.0;
+        c->kcount[k] = 0;
+    }
+    return RR_OK;
+}
+
+int rr_kernel_times(rr_ctx* c, double* ms, uint64_t* launches, int32_t n) {
+    if (!c) return fail(RR_E_ARG, "null context");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    int rc = resolve_prof(c);
+    if (rc != RR_OK) return rc;
+    for (int k = 0; k < n && k < rr::K_COUNT; ++k) {
+        if (ms) ms[k] = c->kms[k];
+        if (launches) launches[k] = c->kcount[k];
+    }
+    return rr::K_COUNT;
+}
+
+int rr_last_stats(rr_ctx* c, rr_stats* s) {
+    if (!c || !s) return fail(RR_E_ARG, "null argument");
+    uint64_t samples = c->last.samples;
+    int rc = finish_stats(c);
+    if (rc != RR_OK) return rc;
+    c->last.samples = samples;
+    *s = c->last;
+    return RR_OK;
+}
+
+int rr_render(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, double* out_canvas, double* out_avg,
+              rr_stats* stats) {
+    if (!c) return fail(RR_E_ARG, "null context");
+    int rc = check_opts(cam, o);
+    if (rc != RR_OK) return rc;
+    const int32_t block = o->block_rows > 0 ? o->block_rows : 8;
+    const int64_t H = cam->vsize / o->aa, W = cam->hsize / o->aa;
+    const int64_t rows = part_rows_count(H, o->part, o->nparts, block);
+    const int64_t total = rows * o->aa * cam->hsize;
+    HIPCHK(hipSetDevice(c->device));
+    const bool want_avg = (o->flags & RR_OUT_AVG) && out_avg;
+    HIPCHK(c->qout.ensure(std::max<int64_t>(W * rows, 1) * 3 * sizeof(double)));
+    rc = rr_render_device(c, cam, o, nullptr, want_avg ? c->qout.p : nullptr, nullptr);
+    if (rc != RR_OK) return rc;
+    if ((o->flags & RR_OUT_CANVAS) && out_canvas)
+        HIPCHK(hipMemcpyAsync(out_canvas, c->canvas.p, total * 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (want_avg)
+        HIPCHK(hipMemcpyAsync(out_avg, c->qout.p, W * rows * 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (stats) return rr_last_stats(c, stats);
+    return RR_OK;
+}
+
+int rr_color_at(rr_ctx* c, int64_t n, const double* origins, const double* directions, int32_t remaining,
+                uint64_t seed, int32_t jitter_mode, double* out_rgb) {
+    if (!c || (n > 0 && (!origins || !directions || !out_rgb))) return fail(RR_E_ARG, "null argument");
+    if (!c->has_scene) return fail(RR_E_ARG, "no scene uploaded");
+    if (remaining < 0 || remaining > RR_MAX_DEPTH) return fail(RR_E_LIMIT, "remaining out of range");
+    if (n == 0) return RR_OK;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    std::vector<double> rays((size_t)n * 6);
+    for (int64_t i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) {
+            rays[6 * i + k] = origins[3 * i + k];
+            rays[6 * i + 3 + k] = directions[3 * i + k];
+        }
+    HIPCHK(upload(c->rays0, rays, st));
+    HIPCHK(c->qout.ensure(n * 3 * sizeof(double)));
+    HIPCHK(hipMemsetAsync(c->counters.p, 0, rr::C_COUNT * sizeof(unsigned long long), st));
+    rr::LevelArgs A{};
+    A.hs = 1;
+    A.aa = 1;
+    A.part = 0;
+    A.nparts = 1;
+    A.block_rows = 1;
+    A.rays0 = c->rays0.as<double>();
+    A.seed = seed;
+    A.jitter_mode = jitter_mode;
+    int rc = run_levels(c, A, n, remaining, c->qout.as<double>());
+    if (rc != RR_OK) return rc;
+    HIPCHK(hipMemcpyAsync(out_rgb, c->qout.p, n * 3 * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return RR_OK;
+}
+
+int rr_is_shadowed(rr_ctx* c, int64_t n, const double* points, const double* light_positions, int32_t* out) {
+    if (!c || (n > 0 && (!points || !light_positions || !out))) return fail(RR_E_ARG, "null argument");
+    if (!c->has_scene) return fail(RR_E_ARG, "no scene uploaded");
+    if (n == 0) return RR_OK;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    std::vector<double> buf((size_t)n * 6);
+    std::memcpy(buf.data(), points, n * 3 * sizeof(double));
+    std::memcpy(buf.data() + 3 * n, light_positions, n * 3 * sizeof(double));
+    HIPCHK(upload(c->rays0, buf, st));
+    HIPCHK(c->qout.ensure(n * sizeof(int32_t)));
+    HIPCHK(rr::launch_shadow_query(c->S, c->rays0.as<double>(), c->rays0.as<double>() + 3 * n, n,
+                                   c->qout.as<int32_t>(), c->counters.as<unsigned long long>(), st));
+    HIPCHK(hipMemcpyAsync(out, c->qout.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return RR_OK;
+}
+
+}  // extern "C"

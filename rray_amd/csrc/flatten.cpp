@@ -1,0 +1,294 @@
+// flatten.cpp — flattens the reference's object registry into the HBM layout.
+//
+// Order: Scene.ids (scene.rs:24-27) with every group's Group.child_ids inlined depth-first.
+// That is the order in which Scene::intersect appends intersections before its stable sort
+// (scene.rs:97-106; group.rs:80-91 sorts its children's hits first, which a stable sort of the
+// concatenation reproduces), so "earliest node index" is the reference's tie-break.
+#include "flatten.hpp"
+
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <limits>
+
+namespace rr {
+
+namespace {
+
+struct Box {
+    Tup min, max;
+};
+
+void adjust_min_max(Box& b, double x, double y, double z) {  // object.rs:220-227 (f64::min/max == fmin/fmax)
+    b.min = point(std::fmin(b.min.x, x), std::fmin(b.min.y, y), std::fmin(b.min.z, z));
+    b.max = point(std::fmax(b.max.x, x), std::fmax(b.max.y, y), std::fmax(b.max.z, z));
+}
+
+Box apply_transform(const Box& b, const M4& m) {  // object.rs:257-278
+    const Tup corners[8] = {point(b.min.x, b.min.y, b.min.z), point(b.min.x, b.min.y, b.max.z),
+                            point(b.min.x, b.max.y, b.min.z), point(b.min.x, b.max.y, b.max.z),
+                            point(b.max.x, b.min.y, b.min.z), point(b.max.x, b.min.y, b.max.z),
+                            point(b.max.x, b.max.y, b.min.z), point(b.max.x, b.max.y, b.max.z)};
+    const double inf = std::numeric_limits<double>::infinity();
+    Box r{point(inf, inf, inf), point(-inf, -inf, -inf)};
+    for (const Tup& c : corners) {
+        Tup t = mul(m, c);
+        adjust_min_max(r, t.x, t.y, t.z);
+    }
+    return r;
+}
+
+M4 load16(const double* p) {
+    M4 m{};
+    for (int i = 0; i < 16; ++i) m.m[i] = p[i];
+    return m;
+}
+
+bool is_identity12(const double* m) {
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 4; ++c)
+            if (m[r * 4 + c] != (r == c ? 1.0 : 0.0)) return false;
+    return true;
+}
+
+}  // namespace
+
+bool inverse_3x4(const M4& transform, const double* given, double out12[12], M4* full, std::string& err) {
+    M4 inv = given ? load16(given) : inverse(transform);
+    if (!(inv.get(3, 0) == 0.0 && inv.get(3, 1) == 0.0 && inv.get(3, 2) == 0.0 && inv.get(3, 3) == 1.0)) {
+        err = "inverse transform is not affine (row 3 != 0,0,0,1)";
+        return false;
+    }
+    for (int i = 0; i < 12; ++i) out12[i] = inv.m[i];
+    if (full) *full = inv;
+    return true;
+}
+
+int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
+    out = HostScene();
+    const int n = d.n_objects;
+    if (n < 0 || (n > 0 && (!d.kind || !d.parent || !d.transform || !d.material))) {
+        err = "scene descriptor: missing per-object arrays";
+        return RR_E_ARG;
+    }
+    if (d.n_top < 0 || (d.n_top > 0 && !d.top)) {
+        err = "scene descriptor: missing top-level id list";
+        return RR_E_ARG;
+    }
+    // materials
+    for (int i = 0; i < d.n_materials; ++i) {
+        DevMaterial m{};
+        const double* p = d.mat + 7 * (size_t)i;
+        m.ambient = p[0];
+        m.diffuse = p[1];
+        m.specular = p[2];
+        m.shininess = p[3];
+        m.reflective = p[4];
+        m.transparency = p[5];
+        m.refractive_index = p[6];
+        m.pattern = d.mat_pattern ? d.mat_pattern[i] : -1;
+        if (m.pattern < -1 || m.pattern >= d.n_patterns) {
+            err = "material references an unknown pattern";
+            return RR_E_ARG;
+        }
+        out.mats.push_back(m);
+    }
+    // patterns
+    for (int i = 0; i < d.n_patterns; ++i) {
+        DevPattern p{};
+        p.kind = d.pat_kind[i];
+        p.a = d.pat_a ? d.pat_a[i] : -1;
+        p.b = d.pat_b ? d.pat_b[i] : -1;
+        for (int c = 0; c < 3; ++c) p.color[c] = d.pat_color ? d.pat_color[3 * (size_t)i + c] : 0.0;
+        p.scale = d.pat_scale ? d.pat_scale[i] : 0.5;
+        M4 t = d.pat_transform ? load16(d.pat_transform + 16 * (size_t)i) : identity();
+        if (!inverse_3x4(t, nullptr, p.inv, nullptr, err)) return RR_E_NONAFFINE;
+        p.flags = is_identity12(p.inv) ? NF_IDENT : 0;
+        if (p.kind < RR_PAT_TEST || p.kind > RR_PAT_BLEND) {
+            err = "unknown pattern kind";
+            return RR_E_ARG;
+        }
+        bool binary = p.kind != RR_PAT_TEST && p.kind != RR_PAT_SOLID;
+        if (binary && (p.a < 0 || p.a >= d.n_patterns || p.b < 0 || p.b >= d.n_patterns)) {
+            err = "pattern child index out of range";
+            return RR_E_ARG;
+        }
+        out.pats.push_back(p);
+    }
+    // pattern nesting depth (the kernel evaluates trees with a bounded explicit stack)
+    std::function<int(int, int)> pdepth = [&](int i, int lvl) -> int {
+        if (lvl > RR_MAX_PATTERN_DEPTH) return lvl;
+        const DevPattern& p = out.pats[i];
+        if (p.kind == RR_PAT_TEST || p.kind == RR_PAT_SOLID) return lvl;
+        return std::max(pdepth(p.a, lvl + 1), pdepth(p.b, lvl + 1));
+    };
+    for (int i = 0; i < d.n_patterns; ++i)
+        if (pdepth(i, 1) > RR_MAX_PATTERN_DEPTH) {
+            err = "pattern nesting exceeds RR_MAX_PATTERN_DEPTH";
+            return RR_E_LIMIT;
+        }
+    // lights
+    for (int i = 0; i < d.n_lights; ++i) {
+        DevLight l{};
+        const double* p = d.light + 15 * (size_t)i;
+        for (int c = 0; c < 3; ++c) {
+            l.position[c] = p[c];
+            l.intensity[c] = p[3 + c];
+            l.corner[c] = p[6 + c];
+            l.u[c] = p[9 + c];
+            l.v[c] = p[12 + c];
+        }
+        l.kind = d.light_kind[i];
+        l.level = d.light_level ? d.light_level[i] : 0;
+        if (l.kind == RR_LIGHT_AREA && l.level <= 0) {
+            err = "area light with level <= 0";
+            return RR_E_SCENE;
+        }
+        out.lights.push_back(l);
+    }
+
+    // objects: per-object inverses, triangle data, group AABBs (cached like group.rs:54-67)
+    std::vector<M4> fwd((size_t)n);
+    std::vector<double> inv12((size_t)n * 12);
+    std::vector<int> tri_index((size_t)n, -1);
+    for (int i = 0; i < n; ++i) {
+        fwd[i] = load16(d.transform + 16 * (size_t)i);
+        if (!inverse_3x4(fwd[i], d.inverse ? d.inverse + 16 * (size_t)i : nullptr, &inv12[12 * (size_t)i], nullptr,
+                         err)) {
+            err = "object " + std::to_string(i) + ": " + err;
+            return RR_E_NONAFFINE;
+        }
+        int k = d.kind[i];
+        if (k < RR_SPHERE || k > RR_SMOOTH_TRIANGLE) {
+            err = "unknown object kind";
+            return RR_E_ARG;
+        }
+        if (k != RR_GROUP && (d.material[i] < 0 || d.material[i] >= d.n_materials)) {
+            err = "object " + std::to_string(i) + " has no valid material";
+            return RR_E_ARG;
+        }
+        if (k == RR_TRIANGLE || k == RR_SMOOTH_TRIANGLE) {
+            if (!d.tri) {
+                err = "triangle without vertex data";
+                return RR_E_ARG;
+            }
+            const double* p = d.tri + 18 * (size_t)i;
+            Tup p1 = point(p[0], p[1], p[2]), p2 = point(p[3], p[4], p[5]), p3 = point(p[6], p[7], p[8]);
+            Tup e1 = p2 - p1, e2 = p3 - p1;  // triangle.rs:52-56
+            Tup nn = normalize(cross(e2, e1));
+            DevTri t{};
+            const double pp[3] = {p1.x, p1.y, p1.z}, a1[3] = {e1.x, e1.y, e1.z}, a2[3] = {e2.x, e2.y, e2.z},
+                         no[3] = {nn.x, nn.y, nn.z};
+            for (int c = 0; c < 3; ++c) {
+                t.p1[c] = pp[c];
+                t.e1[c] = a1[c];
+                t.e2[c] = a2[c];
+                t.normal[c] = no[c];
+                t.n1[c] = p[9 + c];
+                t.n2[c] = p[12 + c];
+                t.n3[c] = p[15 + c];
+            }
+            t.smooth = (k == RR_SMOOTH_TRIANGLE);
+            tri_index[i] = (int)out.tris.size();
+            out.tris.push_back(t);
+        }
+    }
+    const double inf = std::numeric_limits<double>::infinity();
+    std::vector<int> aabb_state((size_t)n, 0);
+    std::vector<Box> aabb((size_t)n);
+    std::function<Box(int, int)> get_aabb = [&](int id, int lvl) -> Box {
+        int k = d.kind[id];
+        if (k == RR_SPHERE) return {point(-1, -1, -1), point(1, 1, 1)};            // sphere.rs get_aabb
+        if (k == RR_PLANE) return {point(-inf, 0.0, -inf), point(inf, 0.0, inf)};  // plane.rs get_aabb
+        if (k != RR_GROUP) {                                                       // triangle.rs get_aabb
+            const double* p = d.tri + 18 * (size_t)id;
+            return {point(std::fmin(p[0], std::fmin(p[3], p[6])), std::fmin(p[1], std::fmin(p[4], p[7])),
+                          std::fmin(p[2], std::fmin(p[5], p[8]))),
+                    point(std::fmax(p[0], std::fmax(p[3], p[6])), std::fmax(p[1], std::fmax(p[4], p[7])),
+                          std::fmax(p[2], std::fmax(p[5], p[8])))};
+        }
+        if (aabb_state[id] == 2) return aabb[id];
+        Box b{point(inf, inf, inf), point(-inf, -inf, -inf)};  // group.rs:128-149
+        int cs = d.child_start ? d.child_start[id] : 0, cc = d.child_count ? d.child_count[id] : 0;
+        for (int j = 0; j < cc && lvl < 64; ++j) {
+            int c = d.children[cs + j];
+            Box cb = apply_transform(get_aabb(c, lvl + 1), fwd[c]);
+            adjust_min_max(b, cb.min.x, cb.min.y, cb.min.z);  // AABB::adjust_aabb (object.rs:237-240)
+            adjust_min_max(b, cb.max.x, cb.max.y, cb.max.z);
+        }
+        aabb[id] = b;
+        aabb_state[id] = 2;
+        return b;
+    };
+
+    // depth-first flattening
+    out.node_of_object.assign((size_t)n, -1);
+    std::vector<int32_t> anc;
+    std::function<int(int, int)> visit = [&](int id, int parent_node) -> int {
+        if (id < 0 || id >= n) {
+            err = "object id out of range";
+            return RR_E_ARG;
+        }
+        if (out.node_of_object[id] != -1) {
+            err = "object " + std::to_string(id) + " appears twice in the scene tree";
+            return RR_E_ARG;
+        }
+        int idx = (int)out.nodes.size();
+        out.node_of_object[id] = idx;
+        DevNode nd{};
+        std::memcpy(nd.inv, &inv12[12 * (size_t)id], sizeof(nd.inv));
+        nd.kind = d.kind[id];
+        nd.flags = is_identity12(nd.inv) ? NF_IDENT : 0;
+        nd.material = nd.kind == RR_GROUP ? -1 : d.material[id];
+        nd.parent = parent_node;
+        nd.depth = (int32_t)anc.size();
+        nd.aux = tri_index[id];
+        if (parent_node >= 0 && d.parent[id] >= 0 && out.node_of_object[d.parent[id]] != parent_node) {
+            err = "object parent link disagrees with the group child list";
+            return RR_E_ARG;
+        }
+        out.nodes.push_back(nd);
+        if (nd.kind == RR_GROUP) {
+            if ((int)anc.size() >= RR_MAX_GROUP_DEPTH) {
+                err = "group nesting exceeds RR_MAX_GROUP_DEPTH";
+                return RR_E_LIMIT;
+            }
+            anc.push_back(idx);
+            DevGroup g{};
+            Box b = get_aabb(id, 0);
+            g.aabb[0] = b.min.x;
+            g.aabb[1] = b.min.y;
+            g.aabb[2] = b.min.z;
+            g.aabb[3] = b.max.x;
+            g.aabb[4] = b.max.y;
+            g.aabb[5] = b.max.z;
+            for (int j = 0; j < RR_MAX_GROUP_DEPTH; ++j) g.anc[j] = j < (int)anc.size() ? anc[j] : -1;
+            g.depth = (int32_t)anc.size();
+            out.nodes[idx].aux = (int)out.groups.size();
+            out.groups.push_back(g);
+            int cs = d.child_start ? d.child_start[id] : 0, cc = d.child_count ? d.child_count[id] : 0;
+            if (cc > 0 && !d.children) {
+                err = "group without children array";
+                return RR_E_ARG;
+            }
+            for (int j = 0; j < cc; ++j) {
+                int rc = visit(d.children[cs + j], idx);
+                if (rc != RR_OK) return rc;
+            }
+            anc.pop_back();
+        } else if (parent_node < 0) {
+            out.n_top_leaves++;
+        }
+        out.nodes[idx].skip = (int)out.nodes.size();
+        return RR_OK;
+    };
+    for (int i = 0; i < d.n_top; ++i) {
+        int rc = visit(d.top[i], -1);
+        if (rc != RR_OK) return rc;
+    }
+    for (const DevNode& nd : out.nodes)
+        if (nd.kind != RR_GROUP && out.mats[nd.material].transparency != 0.0) out.has_transparent = 1;
+    return RR_OK;
+}
+
+}  // namespace rr

@@ -1,0 +1,30 @@
+// flatten.hpp — rr_scene_desc (the reference's object registry) -> HBM layout (rr_device.hpp).
+#pragma once
+#include <string>
+#include <vector>
+
+#include "rr_device.hpp"
+#include "rr_math.hpp"
+
+namespace rr {
+
+struct HostScene {
+    std::vector<DevNode> nodes;
+    std::vector<DevGroup> groups;
+    std::vector<DevTri> tris;
+    std::vector<DevMaterial> mats;
+    std::vector<DevPattern> pats;
+    std::vector<DevLight> lights;
+    std::vector<int32_t> node_of_object;  // object id -> node index (-1 if not in the scene tree)
+    int32_t has_transparent = 0;
+    int64_t n_top_leaves = 0;             // leaves tested by every ray (reference full scan)
+};
+
+// Returns RR_OK or an error code (message in `err`).
+int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err);
+
+// Inverse + affinity check: row 3 of the inverse must be (+-0,+-0,+-0,1) so that a point's w stays
+// exactly 1 and a vector's w stays +-0 (proved for affine inputs in DESIGN.md).
+bool inverse_3x4(const M4& transform, const double* given_inverse, double out12[12], M4* full, std::string& err);
+
+}  // namespace rr

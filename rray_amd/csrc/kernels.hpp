@@ -1,0 +1,67 @@
+// kernels.hpp — host-visible launch interface of render.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <utility>
+#include <vector>
+
+#include "rr_device.hpp"
+#include "wavefront.hpp"
+
+namespace rr {
+
+// Arguments of one wavefront level (see wavefront.hpp).
+struct LevelArgs {
+    DevCamera cam;           // level-0 ray source (when rays0 == nullptr)
+    int64_t hs;              // supersampled width
+    int32_t aa, part, nparts, block_rows;
+    int64_t base;            // first local sample of this batch
+    const double* rays0;     // level-0 explicit rays (o xyz, d xyz); nullptr: camera rays
+    int32_t level, rem;      // level d and `remaining` = max_depth - d
+    int64_t n;               // events at this level
+    const Event* ev;         // level >= 1 input queue
+    HitRec* hit;
+    double* n12;
+    ShadeRec* sr;
+    CombRec* comb;
+    Event* next;
+    int32_t* lit;
+    uint8_t* sb;
+    int32_t* n1n2_list;
+    unsigned int* lcount;    // LC_* (zeroed per level)
+    int32_t n_sr;            // shadow slots per lit hit
+    const int32_t* sr_light;
+    const int32_t* sr_s;
+    uint64_t seed;
+    int32_t jitter_mode;
+    unsigned long long* counters;  // C_* totals
+};
+
+struct CombArgs {
+    int32_t level;
+    int64_t n;
+    int64_t base;
+    const CombRec* comb;
+    CombRec* parent_comb;
+    double* out;  // level 0: canvas (3 doubles per local sample)
+};
+
+// Optional per-kernel timing: when `prof` is non-null every launch is bracketed by HIP events on
+// the launch stream and appended to it (resolved on the host after a synchronise).
+enum KernelId { K_TRACE = 0, K_N1N2, K_SHADE, K_SHADOW, K_FINISH, K_COMBINE, K_AA, K_COUNT };
+struct KernelProf {
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> marks;
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
+    hipEvent_t get();
+};
+
+hipError_t launch_level(const DevScene& S, const LevelArgs& A, int64_t n_sr_upper, hipStream_t stream,
+                        KernelProf* prof = nullptr);
+hipError_t launch_combine(const CombArgs& C, hipStream_t stream, KernelProf* prof = nullptr);
+hipError_t launch_aa(const double* canvas, double* out, int64_t width, int64_t rows, int32_t aa, hipStream_t stream,
+                     KernelProf* prof = nullptr);
+hipError_t launch_shadow_query(const DevScene& S, const double* pts, const double* lps, int64_t n, int32_t* out,
+                               unsigned long long* counters, hipStream_t stream);
+
+}  // namespace rr

@@ -1,0 +1,102 @@
+// rr_device.hpp — the flattened scene as it sits in HBM (shared by host flattener and kernels).
+//
+// The reference keeps Arc<dyn Object> in a mutex-guarded registry (object/db.rs:11-13) and
+// walks it per ray.  Here the registry is flattened once per scene, in Scene.ids order with each
+// group's children inlined (depth-first), which is exactly the tie-break order of the
+// reference's stable sorts (scene.rs:104, group.rs:88).  Every record is read wave-uniformly
+// (all 64 lanes test the same node), so the loads become scalar (SMEM) broadcasts.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/rray/rray.h"
+
+namespace rr {
+
+enum NodeFlags : int32_t {
+    NF_IDENT = 1,  // inverse transform is exactly the identity (skip the ray transform)
+};
+
+// One flattened object.  128 B, 16-B aligned.
+struct alignas(16) DevNode {
+    double inv[12];   // rows 0..2 of the inverse transform (row 3 verified == 0,0,0,1)
+    int32_t kind;     // RR_SPHERE ..
+    int32_t flags;    // NodeFlags
+    int32_t material; // DevMaterial index (leaves)
+    int32_t skip;     // first node index after this node's subtree
+    int32_t parent;   // parent node index (-1 = scene top level)
+    int32_t aux;      // group index (groups) / triangle index (triangles)
+    int32_t depth;    // number of group ancestors
+    int32_t pad;
+};
+static_assert(sizeof(DevNode) == 128, "DevNode layout");
+
+// Per group: bounding box in the group's own space (group.rs:128-149) and its ancestor chain.
+struct alignas(16) DevGroup {
+    double aabb[6];                      // min xyz, max xyz
+    int32_t anc[RR_MAX_GROUP_DEPTH];     // node indices root-first; anc[depth-1] == this group
+    int32_t depth;                       // number of groups from the root down to and incl. this one
+    int32_t pad;
+};
+
+// Per triangle: Möller-Trumbore data (triangle.rs:52-68) + normals.
+struct alignas(16) DevTri {
+    double p1[3], e1[3], e2[3];
+    double normal[3];          // normalize(e2 x e1)
+    double n1[3], n2[3], n3[3];  // smooth-triangle vertex normals
+    int32_t smooth;
+    int32_t pad;
+};
+
+struct alignas(16) DevMaterial {  // material.rs:35-44
+    double ambient, diffuse, specular, shininess, reflective, transparency, refractive_index;
+    int32_t pattern;
+    int32_t pad;
+};
+
+struct alignas(16) DevPattern {  // pattern.rs:23-27
+    double inv[12];
+    double color[3];
+    double scale;
+    int32_t kind, a, b, flags;
+};
+
+struct alignas(16) DevLight {  // light.rs:17-21
+    double position[3];   // area: corner + u*0.5 + v*0.5 (light.rs:41-45)
+    double intensity[3];
+    double corner[3], u[3], v[3];
+    int32_t kind, level;
+};
+
+struct DevCamera {
+    int64_t hsize, vsize;
+    double half_width, half_height, pixel_size;
+    double inv[16];  // full 4x4 inverse of the camera transform (camera.rs:85)
+};
+
+struct DevScene {
+    const DevNode* nodes;
+    const DevGroup* groups;
+    const DevTri* tris;
+    const DevMaterial* mats;
+    const DevPattern* pats;
+    const DevLight* lights;
+    int32_t n_nodes, n_lights;
+    int32_t has_transparent;  // any material with transparency != 0 (enables the n1/n2 walk)
+    int32_t has_groups;
+};
+
+// Per-launch counters (u64, zeroed by the host before each launch).
+enum Counter {
+    C_RAYS = 0,
+    C_SHADOW,
+    C_SHADE,
+    C_N1N2,
+    C_GROUP_TESTS,
+    C_GROUP_HITS,
+    C_SAMPLES,
+    C_PRIM_TESTS,
+    C_WORK,  // work-queue head
+    C_COUNT
+};
+
+}  // namespace rr

@@ -1,0 +1,47 @@
+// wavefront.hpp — per-level ray queues of the wavefront render (host + device view).
+//
+// Scene::color_at recursion (scene.rs:128-336) is evaluated level by level: level d holds every
+// pending color_at(ray, max_depth - d).  Each level runs trace -> [n1/n2 walk] -> shade ->
+// shadow -> finish; children (reflected / refracted rays) are appended to level d+1 with a parent
+// link, and a bottom-up combine pass reproduces shade_hit's summation exactly (scene.rs:172-177).
+#pragma once
+#include <stdint.h>
+
+namespace rr {
+
+// a pending color_at(ray, rem) at level >= 1 (level 0 rays come from the camera or the caller)
+struct alignas(16) Event {
+    double o[3], d[3];
+    uint32_t sample;  // local sample index (this part / batch-relative + base)
+    uint32_t path;    // recursion path code: root 1, reflected child 2p, refracted child 2p+1
+    int32_t parent;   // event index at level - 1
+    int32_t slot;     // 0 = reflected child, 1 = refracted child
+};
+static_assert(sizeof(Event) == 64, "Event layout");
+
+struct alignas(16) HitRec {  // closest hit of an event (first t >= 0 of the sorted xs)
+    double t, u, v;
+    int32_t node;  // -1: miss
+    int32_t k;     // local entry index (sphere t1 = 0, t2 = 1)
+};
+
+struct alignas(16) ShadeRec {  // Computations subset lighting() needs (computations.rs:13-25)
+    double over[3], eyev[3], normalv[3], pcol[3];
+    int32_t material;
+    int32_t pad;
+};
+
+struct alignas(16) CombRec {  // shade_hit's pending sum
+    double surf[3];
+    double refl_res[3];  // color_at(reflect ray) * reflective, or 0
+    double refr_res[3];  // color_at(refract ray) * transparency, or 0
+    double refl, transp, R;
+    int32_t parent;      // event index at level - 1 (-1 at level 0)
+    int32_t flags;       // CF_*
+};
+enum { CF_HIT = 1, CF_REFRACT_CHILD = 2 };
+
+// per-level device counters
+enum { LC_CHILDREN = 0, LC_LIT, LC_N1N2, LC_COUNT };
+
+}  // namespace rr

@@ -1,0 +1,281 @@
+"""Host-side mirror of the reference's render-path interface over the C ABI.
+
+Reference names kept where they exist:
+  Scene::add_light / add_object, Sphere::new, Plane::new, Group::add_child  -> SceneBuilder
+  Camera::new (camera.rs:41) / Camera::render (camera.rs:107)               -> camera(), Renderer.render
+  Scene::color_at (scene.rs:128), Scene::is_shadowed (scene.rs:234)         -> Renderer.color_at / is_shadowed
+  render_scene_from_str / render_scene_from_file (scene_builder_yaml.rs:387,429)
+Every call goes to librray_amd.so's HIP kernels; there is no CPU path.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+DEFAULT_MATERIAL = (0.1, 0.9, 0.9, 200.0, 0.0, 0.0, 1.0)  # material.rs:47-58
+IDENTITY = tuple(float(i == j) for i in range(4) for j in range(4))
+
+
+def _dp(a):
+    return a.ctypes.data_as(_lib._D)
+
+
+def _ip(a):
+    return a.ctypes.data_as(_lib._I)
+
+
+class SceneBuilder:
+    """Programmatic scene with the reference's registry semantics (object/db.rs, scene.rs:24-71)."""
+
+    def __init__(self):
+        self.kind, self.parent, self.material, self.transform, self.tri, self.kids, self.top = [], [], [], [], [], [], []
+        self.mats, self.mat_pattern = [], []
+        self.pat_kind, self.pat_a, self.pat_b, self.pat_color, self.pat_scale, self.pat_transform = [], [], [], [], [], []
+        self.light_kind, self.light, self.light_level = [], [], []
+        self._keep = None
+
+    # --- materials / patterns (material.rs, pattern.rs)
+    def pattern(self, kind, color=(0.0, 0.0, 0.0), a=-1, b=-1, scale=0.5, transform=IDENTITY):
+        self.pat_kind.append(_lib.PAT[kind] if isinstance(kind, str) else int(kind))
+        self.pat_a.append(a)
+        self.pat_b.append(b)
+        self.pat_color.extend(float(x) for x in color)
+        self.pat_scale.append(float(scale))
+        self.pat_transform.extend(float(x) for x in transform)
+        return len(self.pat_kind) - 1
+
+    def new_material(self, mat7=DEFAULT_MATERIAL, pattern=-1):
+        self.mats.extend(float(x) for x in mat7)
+        self.mat_pattern.append(pattern)
+        return len(self.mat_pattern) - 1
+
+    # --- objects
+    def _obj(self, kind, parent, transform, material, pattern, tri=None):
+        oid = len(self.kind)
+        self.kind.append(kind)
+        self.parent.append(parent)
+        if kind == _lib.GROUP:
+            self.material.append(-1)
+        else:
+            self.material.append(material if isinstance(material, int) else self.new_material(
+                material or DEFAULT_MATERIAL, pattern))
+        self.transform.extend(float(x) for x in (transform or IDENTITY))
+        self.tri.extend([float(x) for x in tri] if tri is not None else [0.0] * 18)
+        self.kids.append([])
+        (self.kids[parent] if parent >= 0 else self.top).append(oid)
+        return oid
+
+    def sphere(self, transform=None, material=None, pattern=-1, parent=-1):
+        return self._obj(_lib.SPHERE, parent, transform, material, pattern)
+
+    def plane(self, transform=None, material=None, pattern=-1, parent=-1):
+        return self._obj(_lib.PLANE, parent, transform, material, pattern)
+
+    def group(self, transform=None, parent=-1):
+        return self._obj(_lib.GROUP, parent, transform, None, -1)
+
+    def triangle(self, p1, p2, p3, transform=None, material=None, pattern=-1, parent=-1):
+        return self._obj(_lib.TRIANGLE, parent, transform, material, pattern, list(p1) + list(p2) + list(p3) + [0.0] * 9)
+
+    def smooth_triangle(self, p1, p2, p3, n1, n2, n3, transform=None, material=None, pattern=-1, parent=-1):
+        return self._obj(_lib.SMOOTH_TRIANGLE, parent, transform, material, pattern,
+                         list(p1) + list(p2) + list(p3) + list(n1) + list(n2) + list(n3))
+
+    # --- lights (light.rs:37-45)
+    def point_light(self, position, intensity):
+        self.light_kind.append(_lib.LIGHT_POINT)
+        self.light_level.append(0)
+        self.light.extend([float(x) for x in position] + [float(x) for x in intensity] + [0.0] * 9)
+        return len(self.light_kind) - 1
+
+    def area_light(self, corner, u, v, intensity, level):
+        c, u, v = [float(x) for x in corner], [float(x) for x in u], [float(x) for x in v]
+        center = [(c[k] + u[k] * 0.5) + v[k] * 0.5 for k in range(3)]  # Python floats == f64 ops
+        self.light_kind.append(_lib.LIGHT_AREA)
+        self.light_level.append(int(level))
+        self.light.extend(center + [float(x) for x in intensity] + c + u + v)
+        return len(self.light_kind) - 1
+
+    def desc(self):
+        child_start, child_count, children = [], [], []
+        for ks in self.kids:
+            child_start.append(len(children))
+            child_count.append(len(ks))
+            children.extend(ks)
+        arr = {
+            "kind": np.array(self.kind, np.int32), "parent": np.array(self.parent, np.int32),
+            "transform": np.array(self.transform, np.float64), "material": np.array(self.material, np.int32),
+            "tri": np.array(self.tri, np.float64), "child_start": np.array(child_start, np.int32),
+            "child_count": np.array(child_count, np.int32), "children": np.array(children or [0], np.int32),
+            "top": np.array(self.top or [0], np.int32), "mat": np.array(self.mats or [0.0], np.float64),
+            "mat_pattern": np.array(self.mat_pattern or [0], np.int32),
+            "pat_kind": np.array(self.pat_kind or [0], np.int32), "pat_a": np.array(self.pat_a or [0], np.int32),
+            "pat_b": np.array(self.pat_b or [0], np.int32), "pat_color": np.array(self.pat_color or [0.0], np.float64),
+            "pat_scale": np.array(self.pat_scale or [0.0], np.float64),
+            "pat_transform": np.array(self.pat_transform or [0.0], np.float64),
+            "light_kind": np.array(self.light_kind or [0], np.int32),
+            "light": np.array(self.light or [0.0], np.float64),
+            "light_level": np.array(self.light_level or [0], np.int32),
+        }
+        d = _lib.SceneDesc()
+        d.n_objects = len(self.kind)
+        d.n_top = len(self.top)
+        d.n_materials = len(self.mat_pattern)
+        d.n_patterns = len(self.pat_kind)
+        d.n_lights = len(self.light_kind)
+        for k, v in arr.items():
+            setattr(d, k, _dp(v) if v.dtype == np.float64 else _ip(v))
+        d.inverse = None
+        self._keep = arr
+        return d
+
+
+class YamlScene:
+    """Product front-end: scene_builder_yaml.rs restated in C++ (rr_scene_from_yaml)."""
+
+    def __init__(self, text, width, height, aa=1, obj_root=None):
+        h = C.c_void_p()
+        cam = _lib.Camera()
+        check(lib().rr_scene_from_yaml(text.encode(), obj_root.encode() if obj_root else None, width, height, aa,
+                                       C.byref(h), C.byref(cam)))
+        self.h, self.camera, self.width, self.height, self.aa = h, cam, width, height, aa
+
+    def desc(self):
+        return lib().rr_scene_desc_of(self.h).contents
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().rr_scene_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+def camera(hsize, vsize, field_of_view, transform=None):
+    """Camera::new (camera.rs:41-63); sizes are the supersampled W*aa x H*aa."""
+    cam = _lib.Camera()
+    t = (C.c_double * 16)(*(transform or IDENTITY))
+    check(lib().rr_camera_new(hsize, vsize, field_of_view, t, C.byref(cam)))
+    return cam
+
+
+def part_rows(height, part, nparts, block_rows=8):
+    n = lib().rr_part_rows(height, part, nparts, block_rows, None)
+    if n < 0:
+        check(int(n))
+    out = np.zeros(max(n, 1), np.int64)
+    lib().rr_part_rows(height, part, nparts, block_rows, out.ctypes.data_as(C.POINTER(C.c_int64)))
+    return out[:n]
+
+
+def device_count():
+    n = C.c_int(0)
+    lib().rr_device_count(C.byref(n))
+    return n.value
+
+
+class Renderer:
+    """One gfx950 device context (rr_ctx): scene in HBM + the wavefront kernels."""
+
+    def __init__(self, device=0):
+        self.h = C.c_void_p()
+        check(lib().rr_create(device, C.byref(self.h)))
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().rr_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, scene):
+        d = scene.desc()
+        check(lib().rr_scene_upload(self.h, C.byref(d)))
+        self._scene = scene
+
+    def render(self, cam, aa=1, max_depth=5, seed=0, jitter_mode=0, part=0, nparts=1, block_rows=8, canvas=False,
+               avg=True):
+        """Camera::render -> dict(avg=(rows, W, 3) f64 before `as u8`, canvas=(rows*aa, W*aa, 3), stats)."""
+        o = _lib.RenderOpts(aa, max_depth, seed, jitter_mode, part, nparts, block_rows,
+                            (_lib.RR_OUT_CANVAS if canvas else 0) | (_lib.RR_OUT_AVG if avg else 0))
+        H, W = cam.vsize // aa, cam.hsize // aa
+        rows = len(part_rows(H, part, nparts, block_rows))
+        out_avg = np.zeros((rows, W, 3), np.float64) if avg else None
+        out_canvas = np.zeros((rows * aa, cam.hsize, 3), np.float64) if canvas else None
+        st = _lib.Stats()
+        check(lib().rr_render(self.h, C.byref(cam), C.byref(o), _dp(out_canvas) if canvas else None,
+                              _dp(out_avg) if avg else None, C.byref(st)))
+        return {"avg": out_avg, "canvas": out_canvas, "stats": st.as_dict()}
+
+    def render_device(self, cam, opts, d_canvas, d_avg, stream=None):
+        """Renders into device buffers (ints: device pointers), ordered on `stream` (int or None)."""
+        check(lib().rr_render_device(self.h, C.byref(cam), C.byref(opts), C.c_void_p(d_canvas or 0) if d_canvas else None,
+                                     C.c_void_p(d_avg) if d_avg else None, C.c_void_p(stream) if stream else None))
+
+    def kernel_profile(self, enable=True):
+        check(lib().rr_kernel_profile(self.h, 1 if enable else 0))
+
+    def kernel_times(self):
+        """{kernel: (total_ms, launches)} accumulated since kernel_profile(True)."""
+        ms = (C.c_double * 16)()
+        n = (C.c_uint64 * 16)()
+        k = lib().rr_kernel_times(self.h, ms, n, 16)
+        if k < 0:
+            check(k)
+        return {_lib.KERNELS[i]: (ms[i], int(n[i])) for i in range(k)}
+
+    def last_stats(self):
+        st = _lib.Stats()
+        check(lib().rr_last_stats(self.h, C.byref(st)))
+        return st.as_dict()
+
+    def color_at(self, origins, directions, remaining=5, seed=0, jitter_mode=0):
+        o = np.ascontiguousarray(origins, np.float64).reshape(-1, 3)
+        d = np.ascontiguousarray(directions, np.float64).reshape(-1, 3)
+        out = np.zeros_like(o)
+        check(lib().rr_color_at(self.h, len(o), _dp(o), _dp(d), remaining, seed, jitter_mode, _dp(out)))
+        return out
+
+    def is_shadowed(self, points, light_positions):
+        p = np.ascontiguousarray(points, np.float64).reshape(-1, 3)
+        lp = np.ascontiguousarray(light_positions, np.float64).reshape(-1, 3)
+        out = np.zeros(len(p), np.int32)
+        check(lib().rr_is_shadowed(self.h, len(p), _dp(p), _dp(lp), _ip(out)))
+        return out.astype(bool)
+
+
+def quantize(avg):
+    """canvas.rs:97-100: `(v*255.0) as u8` per channel + alpha 255."""
+    avg = np.ascontiguousarray(avg, np.float64)
+    n = avg.shape[0] * avg.shape[1]
+    out = np.zeros((avg.shape[0], avg.shape[1], 4), np.uint8)
+    check(lib().rr_quantize(_dp(avg), n, out.ctypes.data_as(C.POINTER(C.c_uint8))))
+    return out
+
+
+def write_png(path, rgba):
+    rgba = np.ascontiguousarray(rgba, np.uint8)
+    check(lib().rr_write_png(path.encode(), rgba.ctypes.data_as(C.POINTER(C.c_uint8)), rgba.shape[1], rgba.shape[0]))
+
+
+def render_scene_from_str(text, width, height, png_file, aa=1, device=0, obj_root=None):
+    """scene_builder_yaml.rs:387-410 on the GPU."""
+    s = YamlScene(text, width, height, aa, obj_root)
+    r = Renderer(device)
+    r.upload(s)
+    res = r.render(s.camera, aa=aa)
+    write_png(png_file, quantize(res["avg"]))
+    return res
+
+
+def render_scene_from_file(path, width, height, png_file, aa=1, device=0):
+    """scene_builder_yaml.rs:429-436 on the GPU (same error as the reference for a missing file)."""
+    check(lib().rr_render_scene_from_file(path.encode(), width, height, png_file.encode(), aa, device))

@@ -1,0 +1,149 @@
+"""CPU-side tests of the product library: exports, host logic (YAML front-end, flattening,
+partitioning, quantisation, PNG) — no kernel launches."""
+import ctypes as C
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCENES = os.path.join(ROOT, "scenes")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+@pytest.fixture(scope="module")
+def R():
+    from rray_amd import build
+
+    build.build()
+    import rray_amd
+
+    return rray_amd
+
+
+def header_functions():
+    text = open(os.path.join(ROOT, "include", "rray", "rray.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rr_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol(R):
+    L = R.lib()
+    names = header_functions()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    assert L.rr_abi_version() == 1
+    assert sorted(R._lib.EXPORTS) == names
+
+
+def test_no_cpu_fallback_without_device(R):
+    if R.device_count() > 0:
+        pytest.skip("a GPU is visible; the no-device path is exercised on CPU hosts")
+    with pytest.raises(R.RRError) as e:
+        R.Renderer(0)
+    assert e.value.code == -2  # RR_E_HIP
+
+
+def _inspect(R, desc):
+    n = desc.n_objects
+    inv, aabb, node = np.zeros((n, 16)), np.zeros((n, 6)), np.zeros(n, np.int32)
+    R._lib.check(R.lib().rr_scene_inspect(C.byref(desc), inv.ctypes.data_as(R._lib._D),
+                                          aabb.ctypes.data_as(R._lib._D), node.ctypes.data_as(R._lib._I)))
+    return inv, aabb, node
+
+
+YAMLS = [(SCENES, f) for f in ("c1_readme.yaml", "c2_s1024.yaml", "c3_s1024_reflect.yaml", "c4_teapot.yaml",
+                               "c5_area_light.yaml")] + \
+        [(GOLDEN, f) for f in ("checker_pattern.yaml", "stripe_pattern.yaml", "gradient_pattern.yaml",
+                               "ring_pattern.yaml", "blend_pattern.yaml", "triangle.yaml")]
+
+
+@pytest.mark.parametrize("root,name", YAMLS)
+def test_yaml_front_end_matches_oracle_builder(R, oracle_mod, root, name):
+    """C++ YAML parser + builder vs PyYAML + the oracle's restatement: bit-identical inverses,
+    group boxes and camera (scene_builder_yaml.rs:89-365, matrix.rs:389-412, group.rs:128-149)."""
+    from oracle.scene_yaml import build_from_yaml
+
+    text = open(os.path.join(root, name)).read()
+    s = R.YamlScene(text, 64, 48, 2, obj_root=root)
+    o, cam = build_from_yaml(text, 64, 48, 2, obj_root=root)
+    d = s.desc()
+    inv, aabb, node = _inspect(R, d)
+    assert o.num_objects() == d.n_objects
+    for i in range(d.n_objects):
+        ref = np.array(o.inverse_of(i)).reshape(4, 4)
+        assert np.array_equal(inv[i].reshape(4, 4)[:3], ref[:3]), (name, i)
+        if d.kind[i] == 2:
+            assert np.array_equal(aabb[i], np.array(o.group_aabb(i)), equal_nan=True), (name, i)
+    for f in ("hsize", "vsize", "pixel_size", "half_width", "half_height"):
+        assert getattr(s.camera, f) == getattr(cam, f), f
+    assert list(s.camera.transform) == list(cam.transform)
+
+
+def test_yaml_edge_cases(R):
+    base = "camera:\r  fov: 60\r  from: [0, 1.5, -5.0]\r  to: [0,1,0]\r  up:\r    - 0\r    - 1\r    - 0\r"
+    text = base + ("lights:\r  - type: point  # comment\r    color: [.25, 1e0, 2.5E-1]\r    position: [-10,10,-10]\r"
+                   "scene:\r  - type: sphere\r    transforms:\r      - type: rotate\r        axis: 'y'\r"
+                   "        angle: 30\r  - type: plane\r    hidden: true\r---\rcamera: junk\r")
+    s = R.YamlScene(text, 10, 10, 1)
+    d = s.desc()
+    assert d.n_objects == 1 and d.n_lights == 1
+    assert [d.light[3 + k] for k in range(3)] == [0.25, 1.0, 0.25]
+    assert math.isclose(s.camera.field_of_view, math.pi / 3)
+    with pytest.raises(R.RRError):
+        R.YamlScene(base + "lights: []\rscene: []\r", 10, 10, 1)  # "No lights found in scene"
+    with pytest.raises(R.RRError):
+        R.YamlScene(base + "lights:\r  - type: spot\r    color: [1,1,1]\rscene: []\r", 10, 10, 1)
+    with pytest.raises(R.RRError) as e:
+        R.YamlScene(base + "lights:\r  - type: point\r    color: [1,1,1]\r    position: [0,0,0]\r"
+                    "scene:\r  - type: cube\r", 10, 10, 1)
+    assert e.value.code == -5  # RR_E_LIMIT: out-of-scope shape, reported not silently dropped
+
+
+def test_obj_loader_counts(R):
+    text = ("camera: {fov: 60, from: [0, 0, -5], to: [0, 0, 0], up: [0, 1, 0]}\nlights:\n  - type: point\n"
+            "    color: [1, 1, 1]\n    position: [0, 0, -5]\nscene:\n  - type: obj_file\n    obj_file: OBJ\n")
+    s = R.YamlScene(text.replace("OBJ", "teapot-low.obj"), 8, 8, 1, obj_root=GOLDEN)
+    d = s.desc()
+    assert d.n_objects == 241 and d.kind[0] == 2 and d.child_count[0] == 240  # load_obj.rs:153-158
+    s = R.YamlScene(text.replace("OBJ", "triangles.obj"), 8, 8, 1, obj_root=GOLDEN)
+    d = s.desc()  # two all-triangle models: tobj leaves face_arities empty -> empty groups
+    assert d.n_objects == 3 and all(d.child_count[i] == 0 for i in (1, 2))
+
+
+def test_partition_rows(R):
+    for H in (1, 7, 1080, 2160):
+        for n in (1, 2, 3, 4, 8):
+            allrows = np.concatenate([R.part_rows(H, p, n, 8) for p in range(n)])
+            assert np.array_equal(np.sort(allrows), np.arange(H)), (H, n)
+
+
+def test_quantize_and_png(R, oracle_mod, tmp_path):
+    rng = np.random.default_rng(0)
+    avg = rng.uniform(-0.2, 1.3, (5, 7, 3))
+    avg[0, 0] = [np.nan, np.inf, -np.inf]
+    q = R.quantize(avg)
+    assert np.array_equal(q, oracle_mod.Oracle.quantize(avg))
+    assert list(q[0, 0]) == [0, 255, 0, 255]
+    p = str(tmp_path / "x.png")
+    R.write_png(p, q)
+    from PIL import Image
+
+    assert np.array_equal(np.array(Image.open(p).convert("RGBA")), q)
+
+
+def test_camera_new_matches_oracle(R, oracle_mod):
+    M = oracle_mod.Oracle.mat
+    t = M.view_transform((0, 1.5, -5), (0, 1, 0), (0, 1, 0))
+    for hs, vs in ((160, 120), (125, 200), (1920, 1080)):
+        a = R.camera(hs, vs, math.pi / 3, t)
+        b = oracle_mod.Oracle.camera(hs, vs, math.pi / 3, t)
+        assert (a.pixel_size, a.half_width, a.half_height) == (b.pixel_size, b.half_width, b.half_height)
+
+
+def test_jitter_is_deterministic_and_uniform(oracle_mod):
+    v = np.array([oracle_mod.Oracle.jitter(0, s, 1, 0, k, 0) for s in range(200) for k in range(25)])
+    assert v.min() >= 0 and v.max() < 1 and abs(v.mean() - 0.5) < 0.02
