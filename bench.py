@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c2_s1024", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-stride", type=int, default=4, help="CPU sample: one 8-row band in every STRIDE bands")
+    ap.add_argument("--cpu-stride", type=int, default=1, help="CPU sample: one 8-row band in every STRIDE bands")
     args = ap.parse_args()
 
     import numpy as np
@@ -75,14 +75,15 @@ def main():
     max_rows = max(len(R.part_rows(H, p, world, block)) for p in range(world))
     dev = torch.device("cuda", local)
     tile = torch.zeros((max_rows, W, 3), dtype=torch.float64, device=dev)
-    gather = [torch.empty_like(tile) for _ in range(world)] if (world > 1 and rank == 0) else None
+    frame = torch.empty((H, W, 3), dtype=torch.float64, device=dev) if (world > 1 and rank == 0) else None
+    from rray_amd import dist as rdist
     opts = R._lib.RenderOpts(aa, depth, 0, 0, rank, world, block, R._lib.RR_OUT_AVG)
 
     def step():
         stream = torch.cuda.current_stream(dev).cuda_stream
         rend.render_device(cam, opts, None, tile.data_ptr(), stream)
         if world > 1:
-            dist.gather(tile, gather_list=gather, dst=0)
+            rdist.gather_frame(tile, H, block, out=frame)
 
     def sync():
         torch.cuda.synchronize(dev)

@@ -1,0 +1,25 @@
+#!/bin/bash
+# rocprofv3 session for the bench workload: kernel-trace stats, then one PMC pass per counter group
+# (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950).  No --sys-trace / runtime trace with --pmc.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOTDIR=$(pwd)
+OUT=$ROOTDIR/gpurun_out/prof
+WL=${WL:-c2_s1024}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+python -c "import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1 || exit 1
+run() {  # name, timeout, rocprof args...
+  local name=$1 t=$2; shift 2
+  echo "== $name ($(date +%T))"
+  (cd /tmp && timeout -k 10 "$t" rocprofv3 "$@" -d "$OUT/$name" -o run --output-format csv -- \
+      python3 "$ROOTDIR/bench.py" --workload "$WL" --steps 5 --warmup 1 --no-cpu-baseline) > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -n 3 "$OUT/$name.log"
+  return $rc
+}
+run kt 300 --kernel-trace --stats || exit 1
+run pmc_fetch 300 --pmc FETCH_SIZE || exit 1
+run pmc_write 300 --pmc WRITE_SIZE || exit 1
+run pmc_sq 300 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES || exit 1
+find "$OUT" -name "*.csv" | head -50
