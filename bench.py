@@ -113,18 +113,14 @@ def main():
     # roofline of the dominant kernel (rank 0's measurements)
     dom = max(ktimes, key=lambda k: ktimes[k][0])
     dom_ms, dom_n = ktimes[dom]
-    per_ray = (FLOPS["sphere"] * counts["sphere"] + FLOPS["plane"] * counts["plane"] + FLOPS["group"] * counts["group"])
-    if dom == "trace":
-        units = stats["rays"]  # closest-hit rays of one frame = launches' rays (full scan, no early exit)
-        flops = units * per_ray + (FLOPS["tri"] * stats["prim_tests"] if counts["tri"] else 0)
-    elif dom == "shadow":
-        units = stats["shadow_rays"]
-        flops = units * per_ray
+    walk = {"trace": 0, "shadow": 1, "n1n2": 2}
+    if dom in walk:  # f64 flops of the exact tests this kernel executed after culling (last step)
+        flops = stats["exact_flops"][walk[dom]]
     else:
-        units = stats["shade_events"]
-        flops = units * FLOPS["shade"]
+        flops = stats["shade_events"] * FLOPS["shade"]
     launches_per_frame = dom_n / args.steps
-    achieved = flops / launches_per_frame / (dom_ms / dom_n / 1e3) / 1e12 if dom_ms > 0 else 0.0
+    # flops of one step / (this kernel's time per step) == per-launch flops / average launch duration
+    achieved = flops / (dom_ms / args.steps / 1e3) / 1e12 if dom_ms > 0 else 0.0
     traffic = None
     pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
     if os.path.exists(pmc):
@@ -136,8 +132,10 @@ def main():
                 "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": traffic, "kernel": dom,
                 "kernel_ms": round(dom_ms / dom_n, 4), "launches_per_step": launches_per_frame,
                 "flops_per_launch": flops / launches_per_frame,
-                "note": "FP64 VALU-bound; peak = MI355X FP64 vector = FP64 MFMA dense 78.6 TF; bit-parity forbids "
-                        "FMA contraction so at most half of it is reachable (DESIGN.md §4)"}
+                "note": "achieved = f64 flops of the exact leaf tests the kernel executed (SURVEY §8d model: "
+                        "sphere 57, plane 13, triangle/group 45) / kernel time; the f32 bundle/line culling that "
+                        "removes the other tests is overhead, not counted. Peak = MI355X FP64 vector = FP64 MFMA "
+                        "dense 78.6 TF; bit-parity forbids FMA contraction (DESIGN.md §4)"}
 
     cpu = None
     parity = None
@@ -173,7 +171,8 @@ def main():
                            "parallelism": f"row-tiles x{world}" + (" + rccl gather" if world > 1 else "")},
                 "roofline": roofline, "cpu_baseline": cpu, "parity_sample": parity,
                 "kernels_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in ktimes.items() if v[1]},
-                "stats_last_step": {k: stats[k] for k in ("rays", "shadow_rays", "shade_events", "n1n2_scans")}}
+                "stats_last_step": {k: stats[k] for k in ("rays", "shadow_rays", "shade_events", "n1n2_scans",
+                                                          "prim_tests", "exact_flops", "wave_visits")}}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

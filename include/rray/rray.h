@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 1
+#define RR_ABI_VERSION 2
 
 /* error codes */
 #define RR_OK 0
@@ -115,8 +115,10 @@ typedef struct {
     uint64_t n1n2_scans;    /* prepare_computations container walks (transparent hits) */
     uint64_t group_tests, group_hits;
     uint64_t samples;       /* pixel x AA samples rendered */
-    uint64_t prim_tests;    /* reference-equivalent leaf tests */
+    uint64_t prim_tests;    /* exact f64 leaf tests executed (lane-level, after culling) */
     double kernel_ms;       /* render + AA kernels, HIP events */
+    uint64_t exact_flops[3];  /* f64 flops of those tests (SURVEY §8d model) per walk: trace, shadow, n1n2 */
+    uint64_t wave_visits[3];  /* wave-level node visits (exact test issued for a 64-lane wave), same order */
 } rr_stats;
 
 typedef struct rr_ctx rr_ctx;

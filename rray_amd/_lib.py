@@ -7,6 +7,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "librray_amd.so")
+if os.environ.get("RRAY_LIB"):  # experiment builds (build.build_variant); the default is the in-tree product
+    LIB_PATH = os.environ["RRAY_LIB"]
 HEADER = os.path.join(os.path.dirname(HERE), "include", "rray", "rray.h")
 
 RR_OK = 0
@@ -45,10 +47,15 @@ class RenderOpts(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("shade_events", C.c_uint64),
                 ("n1n2_scans", C.c_uint64), ("group_tests", C.c_uint64), ("group_hits", C.c_uint64),
-                ("samples", C.c_uint64), ("prim_tests", C.c_uint64), ("kernel_ms", C.c_double)]
+                ("samples", C.c_uint64), ("prim_tests", C.c_uint64), ("kernel_ms", C.c_double),
+                ("exact_flops", C.c_uint64 * 3), ("wave_visits", C.c_uint64 * 3)]
 
     def as_dict(self):
-        return {n: getattr(self, n) for n, _ in self._fields_}
+        out = {}
+        for n, _ in self._fields_:
+            v = getattr(self, n)
+            out[n] = list(v) if isinstance(v, C.Array) else v
+        return out
 
 
 EXPORTS = ["rr_abi_version", "rr_last_error", "rr_device_count", "rr_create", "rr_destroy", "rr_scene_upload",

@@ -49,6 +49,31 @@ def _compile(src, deps_mtime, verbose):
     return out
 
 
+def build_variant(name, defines, verbose=False):
+    """Experiment build (e.g. RR_STAMPS phase timers) into rray_amd/_exp/<name>/librray_amd.so; select it
+    at run time with RRAY_LIB=<path>.  Never used by the product path."""
+    out_dir = os.path.join(HERE, "_exp", name)
+    os.makedirs(out_dir, exist_ok=True)
+    flags = ["-D" + d for d in defines]
+    objs = []
+    for src in SOURCES:
+        o = os.path.join(out_dir, os.path.splitext(src)[0] + ".o")
+        pre = [HIPCC, "-x", "hip"] if src.endswith(".cpp") else [HIPCC]
+        cmd = pre + COMMON + DEVICE + flags + ["-c", os.path.join(CSRC, src), "-o", o]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {src}\n{r.stderr}")
+        objs.append(o)
+    lib = os.path.join(out_dir, "librray_amd.so")
+    r = subprocess.run([HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", lib] + objs + ["-lz"], capture_output=True,
+                       text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed\n{r.stderr}")
+    return lib
+
+
 def build(verbose=False, jobs=None):
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
@@ -74,4 +99,7 @@ def build(verbose=False, jobs=None):
 
 
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv))
+    if len(sys.argv) > 2 and sys.argv[1] == "variant":
+        print(build_variant(sys.argv[2], sys.argv[3:]))
+    else:
+        print(build(verbose="-v" in sys.argv))

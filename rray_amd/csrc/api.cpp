@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -63,7 +64,7 @@ struct rr_ctx {
     bool has_scene = false;
     rr::HostScene host;
     rr::DevScene S{};
-    DBuf nodes, groups, tris, mats, pats, lights, sr_light, sr_s;
+    DBuf culls, nodes, groups, tris, mats, pats, lights, sr_light, sr_s;
     int32_t n_sr = 0;
     // workspace
     DBuf counters, lcount, hit, n12, sr, lit, sb, n1n2, ev_a, ev_b, canvas, rays0, qout;
@@ -125,6 +126,8 @@ int64_t part_rows_count(int64_t height, int32_t part, int32_t nparts, int32_t bl
 
 // Runs the wavefront levels for `total` level-0 events; level-0 rays come from the camera or from
 // ctx->rays0 (color_at).  Results (color_at values) land in `out` (3 doubles per event).
+constexpr size_t kCounterBytes = (size_t)rr::RR_CNT_SLOTS * rr::RR_CNT_STRIDE * sizeof(unsigned long long);
+
 int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max_depth, double* out) {
     hipStream_t st = c->stream;
     const int64_t B = std::max<int64_t>(1, c->batch);
@@ -166,7 +169,31 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             A.sr_light = c->sr_light.as<int32_t>();
             A.sr_s = c->sr_s.as<int32_t>();
             A.counters = c->counters.as<unsigned long long>();
+            A.stamps = nullptr;
+#ifdef RR_STAMPS
+            // experiment builds: per-wave phase timers of level 0 of the first batch -> $RRAY_STAMPS
+            const char* stamp_path = std::getenv("RRAY_STAMPS");
+            static DBuf stamp_buf;
+            const size_t stamp_bytes = (size_t)2 * (1 << 16) * 8 * sizeof(unsigned long long);
+            A.stamps = nullptr;
+            if (stamp_path && d == 0 && base == 0) {
+                HIPCHK(stamp_buf.ensure(stamp_bytes));
+                HIPCHK(hipMemsetAsync(stamp_buf.p, 0, stamp_bytes, st));
+                A.stamps = stamp_buf.as<unsigned long long>();
+            }
+#endif
             HIPCHK(rr::launch_level(c->S, A, n * (int64_t)c->n_sr, st, c->profile ? &c->prof : nullptr));
+#ifdef RR_STAMPS
+            if (A.stamps) {
+                std::vector<unsigned long long> hv(stamp_bytes / sizeof(unsigned long long));
+                HIPCHK(hipMemcpyAsync(hv.data(), stamp_buf.p, stamp_bytes, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+                if (FILE* fp = std::fopen(stamp_path, "wb")) {
+                    std::fwrite(hv.data(), 1, stamp_bytes, fp);
+                    std::fclose(fp);
+                }
+            }
+#endif
             level_n.push_back(n);
             if (!children_possible) break;
             HIPCHK(hipMemcpyAsync(c->h_lcount, c->lcount.p, rr::LC_COUNT * sizeof(unsigned int), hipMemcpyDeviceToHost,
@@ -185,6 +212,8 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             C.comb = c->comb[d].as<rr::CombRec>();
             C.parent_comb = d > 0 ? c->comb[d - 1].as<rr::CombRec>() : nullptr;
             C.out = out;
+            C.hs = base_args.hs;
+            C.lrows = base_args.rays0 ? 0 : base_args.lrows;
             HIPCHK(rr::launch_combine(C, st, c->profile ? &c->prof : nullptr));
         }
     }
@@ -193,7 +222,9 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
 
 void collect_stats(rr_ctx* c, rr_stats* s) {
     std::memset(s, 0, sizeof(*s));
-    const unsigned long long* h = c->h_counters;
+    unsigned long long h[rr::RR_CNT_STRIDE] = {};
+    for (int sl = 0; sl < rr::RR_CNT_SLOTS; ++sl)
+        for (int k = 0; k < rr::C_COUNT; ++k) h[k] += c->h_counters[sl * rr::RR_CNT_STRIDE + k];
     s->rays = h[rr::C_RAYS];
     s->shadow_rays = h[rr::C_SHADOW];
     s->shade_events = h[rr::C_SHADE];
@@ -202,6 +233,10 @@ void collect_stats(rr_ctx* c, rr_stats* s) {
     s->group_hits = h[rr::C_GROUP_HITS];
     s->samples = h[rr::C_SAMPLES];
     s->prim_tests = h[rr::C_PRIM_TESTS];
+    for (int k = 0; k < 3; ++k) {
+        s->exact_flops[k] = h[rr::C_FLOPS_TRACE + k];
+        s->wave_visits[k] = h[rr::C_VISITS_TRACE + k];
+    }
 }
 
 int resolve_prof(rr_ctx* c) {
@@ -262,8 +297,8 @@ int rr_create(int device, rr_ctx** out) {
     if (e == hipSuccess) e = hipEventCreate(&c->e1);
     if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_lcount, 64 * sizeof(unsigned int), hipHostMallocDefault);
     if (e == hipSuccess)
-        e = hipHostMalloc((void**)&c->h_counters, rr::C_COUNT * sizeof(unsigned long long), hipHostMallocDefault);
-    if (e == hipSuccess) e = c->counters.ensure(rr::C_COUNT * sizeof(unsigned long long));
+        e = hipHostMalloc((void**)&c->h_counters, kCounterBytes, hipHostMallocDefault);
+    if (e == hipSuccess) e = c->counters.ensure(kCounterBytes);
     if (e == hipSuccess) e = c->lcount.ensure(64 * sizeof(unsigned int));
     if (e != hipSuccess) {
         rr_destroy(c);
@@ -277,7 +312,7 @@ void rr_destroy(rr_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (DBuf* b : {&c->nodes, &c->groups, &c->tris, &c->mats, &c->pats, &c->lights, &c->sr_light, &c->sr_s,
+    for (DBuf* b : {&c->culls, &c->nodes, &c->groups, &c->tris, &c->mats, &c->pats, &c->lights, &c->sr_light, &c->sr_s,
                     &c->counters, &c->lcount, &c->hit, &c->n12, &c->sr, &c->lit, &c->sb, &c->n1n2, &c->ev_a, &c->ev_b,
                     &c->canvas, &c->rays0, &c->qout})
         b->release();
@@ -299,6 +334,7 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     if (rc != RR_OK) return fail(rc, err);
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
+    HIPCHK(upload(c->culls, hs.culls, st));
     HIPCHK(upload(c->nodes, hs.nodes, st));
     HIPCHK(upload(c->groups, hs.groups, st));
     HIPCHK(upload(c->tris, hs.tris, st));
@@ -321,6 +357,7 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     c->n_sr = (int32_t)sl.size();
     c->host = std::move(hs);
     rr::DevScene& S = c->S;
+    S.culls = c->culls.as<rr::DevCull>();
     S.nodes = c->nodes.as<rr::DevNode>();
     S.groups = c->groups.as<rr::DevGroup>();
     S.tris = c->tris.as<rr::DevTri>();
@@ -331,6 +368,7 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     S.n_lights = (int32_t)c->host.lights.size();
     S.has_transparent = c->host.has_transparent;
     S.has_groups = c->host.groups.empty() ? 0 : 1;
+    S.lds_culls = (S.n_nodes <= rr::RR_LDS_CULL_CAP && !std::getenv("RRAY_GLOBAL_CULLS")) ? 1 : 0;
     c->has_scene = true;
     return RR_OK;
 }
@@ -424,11 +462,12 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
         HIPCHK(c->canvas.ensure(std::max<int64_t>(total, 1) * 3 * sizeof(double)));
         canvas = c->canvas.as<double>();
     }
-    HIPCHK(hipMemsetAsync(c->counters.p, 0, rr::C_COUNT * sizeof(unsigned long long), st));
+    HIPCHK(hipMemsetAsync(c->counters.p, 0, kCounterBytes, st));
     HIPCHK(hipEventRecord(c->e0, st));
     rr::LevelArgs A{};
     A.cam = dev_camera(cam);
     A.hs = cam->hsize;
+    A.lrows = local_rows;
     A.aa = o->aa;
     A.part = o->part;
     A.nparts = o->nparts;
@@ -442,7 +481,7 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
         HIPCHK(rr::launch_aa(canvas, static_cast<double*>(d_avg), W, rows, o->aa, st,
                              c->profile ? &c->prof : nullptr));
     HIPCHK(hipEventRecord(c->e1, st));
-    HIPCHK(hipMemcpyAsync(c->h_counters, c->counters.p, rr::C_COUNT * sizeof(unsigned long long),
+    HIPCHK(hipMemcpyAsync(c->h_counters, c->counters.p, kCounterBytes,
                           hipMemcpyDeviceToHost, st));
     if (hip_stream) {  // the caller's stream waits for the tile
         HIPCHK(hipEventRecord(ready, st));
@@ -451,7 +490,6 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     }
     c->stats_pending = true;
     // C_SAMPLES is not incremented by the wavefront kernels; it is the level-0 event count
-    c->h_counters[rr::C_SAMPLES] = 0;
     c->last.samples = (uint64_t)total;
     return RR_OK;
 }
@@ -530,7 +568,7 @@ int rr_color_at(rr_ctx* c, int64_t n, const double* origins, const double* direc
         }
     HIPCHK(upload(c->rays0, rays, st));
     HIPCHK(c->qout.ensure(n * 3 * sizeof(double)));
-    HIPCHK(hipMemsetAsync(c->counters.p, 0, rr::C_COUNT * sizeof(unsigned long long), st));
+    HIPCHK(hipMemsetAsync(c->counters.p, 0, kCounterBytes, st));
     rr::LevelArgs A{};
     A.hs = 1;
     A.aa = 1;

@@ -51,6 +51,63 @@ bool is_identity12(const double* m) {
     return true;
 }
 
+// largest singular value of the upper 3x3 of m: sqrt of the largest eigenvalue of A^T A
+// (cyclic Jacobi on the symmetric 3x3; converges to full double precision)
+double sigma_max(const M4& m) {
+    double A[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double s = 0.0;
+            for (int k = 0; k < 3; ++k) s += m.get(k, i) * m.get(k, j);
+            A[i][j] = s;
+        }
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        double off = std::fabs(A[0][1]) + std::fabs(A[0][2]) + std::fabs(A[1][2]);
+        if (off <= 1e-300) break;
+        for (int p = 0; p < 2; ++p)
+            for (int q = p + 1; q < 3; ++q) {
+                if (A[p][q] == 0.0) continue;
+                double theta = (A[q][q] - A[p][p]) / (2.0 * A[p][q]);
+                double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+                double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < 3; ++k) {  // A = J^T A J
+                    double akp = A[k][p], akq = A[k][q];
+                    A[k][p] = c * akp - s * akq;
+                    A[k][q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < 3; ++k) {
+                    double apk = A[p][k], aqk = A[q][k];
+                    A[p][k] = c * apk - s * aqk;
+                    A[q][k] = s * apk + c * aqk;
+                }
+            }
+    }
+    double mx = std::fmax(A[0][0], std::fmax(A[1][1], A[2][2]));
+    return std::sqrt(std::fmax(mx, 0.0));
+}
+
+// bounding sphere (centre in parent space, radius) of node content with local bound (lc, lr)
+DevCull make_cull(const M4& fwd, const double lc[3], double lr) {
+    DevCull c{};
+    const double inf = std::numeric_limits<double>::infinity();
+    Tup w = mul(fwd, point(lc[0], lc[1], lc[2]));
+    double r = lr * sigma_max(fwd);
+    double scale = std::fabs(w.x) + std::fabs(w.y) + std::fabs(w.z) + r;
+    // relative 1e-3 + absolute terms: covers the f32 rounding of the centre / radius, the gap
+    // between the computed inverse and the exact one, and the f64 test's rounding near tangency
+    r = r * 1.001 + 1e-6 * (1.0 + scale);
+    if (!std::isfinite(w.x) || !std::isfinite(w.y) || !std::isfinite(w.z) || !std::isfinite(r) || lr == inf) {
+        c.c[0] = c.c[1] = c.c[2] = 0.0f;
+        c.r = std::numeric_limits<float>::infinity();
+        return c;
+    }
+    c.c[0] = (float)w.x;
+    c.c[1] = (float)w.y;
+    c.c[2] = (float)w.z;
+    c.r = (float)r * 1.0001f;
+    return c;
+}
+
 }  // namespace
 
 bool inverse_3x4(const M4& transform, const double* given, double out12[12], M4* full, std::string& err) {
@@ -288,6 +345,51 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
     }
     for (const DevNode& nd : out.nodes)
         if (nd.kind != RR_GROUP && out.mats[nd.material].transparency != 0.0) out.has_transparent = 1;
+    // culling bounds (parent space) per node
+    std::vector<int> obj_of_node(out.nodes.size(), -1);
+    for (int i = 0; i < n; ++i)
+        if (out.node_of_object[i] >= 0) obj_of_node[out.node_of_object[i]] = i;
+    out.culls.resize(out.nodes.size());
+    for (size_t ni = 0; ni < out.nodes.size(); ++ni) {
+        const int id = obj_of_node[ni];
+        const DevNode& nd = out.nodes[ni];
+        double lc[3] = {0.0, 0.0, 0.0};
+        double lr = inf;
+        if (nd.kind == RR_SPHERE) {
+            lr = 1.0;
+        } else if (nd.kind == RR_TRIANGLE || nd.kind == RR_SMOOTH_TRIANGLE) {
+            const double* p = d.tri + 18 * (size_t)id;
+            for (int k = 0; k < 3; ++k) lc[k] = (p[k] + p[3 + k] + p[6 + k]) / 3.0;
+            lr = 0.0;
+            for (int v = 0; v < 3; ++v) {
+                double dx = p[3 * v] - lc[0], dy = p[3 * v + 1] - lc[1], dz = p[3 * v + 2] - lc[2];
+                lr = std::fmax(lr, std::sqrt(dx * dx + dy * dy + dz * dz));
+            }
+            lr = lr * 1.001 + 1e-9;
+        } else if (nd.kind == RR_GROUP) {
+            const double* b = out.groups[nd.aux].aabb;
+            bool finite = true;
+            for (int k = 0; k < 6; ++k) finite = finite && std::isfinite(b[k]);
+            if (finite && b[0] <= b[3] && b[1] <= b[4] && b[2] <= b[5]) {
+                for (int k = 0; k < 3; ++k) lc[k] = 0.5 * (b[k] + b[3 + k]);
+                double hx = 0.5 * (b[3] - b[0]), hy = 0.5 * (b[4] - b[1]), hz = 0.5 * (b[5] - b[2]);
+                lr = std::sqrt(hx * hx + hy * hy + hz * hz) * 1.001 + 1e-9;
+            } else if (finite) {
+                lr = 0.0;  // empty group: nothing inside can be hit; a tiny sphere is still conservative
+            }
+        }
+        // world-space bound of the set the kernel's test accepts: the kernel applies the ancestors'
+        // and the node's stored inverses, so map back through their inverses (root-first product)
+        M4 world = identity();
+        std::vector<int> chain;
+        for (int a = (int)ni; a >= 0; a = out.nodes[a].parent) chain.push_back(a);
+        for (int k = (int)chain.size() - 1; k >= 0; --k) {
+            M4 nfull = identity();
+            for (int e = 0; e < 12; ++e) nfull.m[e] = out.nodes[chain[k]].inv[e];
+            world = multiply(world, inverse(nfull));
+        }
+        out.culls[ni] = make_cull(world, lc, lr);
+    }
     return RR_OK;
 }
 

@@ -10,6 +10,7 @@ namespace rr {
 
 struct HostScene {
     std::vector<DevNode> nodes;
+    std::vector<DevCull> culls;  // one per node
     std::vector<DevGroup> groups;
     std::vector<DevTri> tris;
     std::vector<DevMaterial> mats;

@@ -14,6 +14,7 @@ namespace rr {
 struct LevelArgs {
     DevCamera cam;           // level-0 ray source (when rays0 == nullptr)
     int64_t hs;              // supersampled width
+    int64_t lrows;           // part-local supersampled rows (level-0 camera rays run in 8x8 tiles)
     int32_t aa, part, nparts, block_rows;
     int64_t base;            // first local sample of this batch
     const double* rays0;     // level-0 explicit rays (o xyz, d xyz); nullptr: camera rays
@@ -35,6 +36,7 @@ struct LevelArgs {
     uint64_t seed;
     int32_t jitter_mode;
     unsigned long long* counters;  // C_* totals
+    unsigned long long* stamps;    // RR_STAMPS experiment builds only: per-wave phase timers (else null)
 };
 
 struct CombArgs {
@@ -44,7 +46,25 @@ struct CombArgs {
     const CombRec* comb;
     CombRec* parent_comb;
     double* out;  // level 0: canvas (3 doubles per local sample)
+    int64_t hs, lrows;  // lrows > 0: level-0 events are in tile order (tile_to_local)
 };
+
+// Level-0 camera events run in 8x8-sample tiles of the part-local supersampled canvas (8-row bands,
+// 8-column tiles inside a band; the last band / column may be narrower) so that a wave's 64 rays
+// form a tight bundle for the culling in walk_nodes.  Maps tile-order index t to the row-major
+// local sample index (a bijection on [0, hs*lrows)).
+__host__ __device__ inline int64_t tile_to_local(int64_t t, int64_t hs, int64_t lrows) {
+    const int64_t band = t / (8 * hs);
+    int64_t k = t - band * 8 * hs;
+    const int64_t y0 = band * 8;
+    const int64_t hb = lrows - y0 < 8 ? lrows - y0 : 8;
+    const int64_t tc = k / (8 * hb);
+    k -= tc * 8 * hb;
+    const int64_t x0 = tc * 8;
+    const int64_t wc = hs - x0 < 8 ? hs - x0 : 8;
+    const int64_t dy = k / wc;
+    return (y0 + dy) * hs + x0 + (k - dy * wc);
+}
 
 // Optional per-kernel timing: when `prof` is non-null every launch is bracketed by HIP events on
 // the launch stream and appended to it (resolved on the host after a synchronise).

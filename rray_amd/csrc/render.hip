@@ -44,6 +44,11 @@ __device__ Ray camera_ray(const DevCamera& C, int64_t px, int64_t py) {
     return {mk(ow[0], ow[1], ow[2]), mk(dx / mag, dy / mag, dz / mag)};
 }
 
+// row-major local sample index of level-0 event i (camera events run in tile order)
+__device__ __forceinline__ int64_t level0_local(const LevelArgs& A, int64_t i) {
+    return (A.rays0 || A.lrows <= 0) ? A.base + i : tile_to_local(A.base + i, A.hs, A.lrows);
+}
+
 // the ray of event i at this level
 __device__ __forceinline__ Ray event_ray(const LevelArgs& A, int64_t i) {
     if (A.level > 0) {
@@ -55,12 +60,12 @@ __device__ __forceinline__ Ray event_ray(const LevelArgs& A, int64_t i) {
         return {mk(p[0], p[1], p[2]), mk(p[3], p[4], p[5])};
     }
     int64_t px, py;
-    local_to_pixel(A, A.base + i, px, py);
+    local_to_pixel(A, level0_local(A, i), px, py);
     return camera_ray(A.cam, px, py);
 }
 // jitter identity of event i: (global sample id, recursion path)
 __device__ __forceinline__ void event_key(const LevelArgs& A, int64_t i, uint64_t& sample, uint32_t& path) {
-    int64_t ls = A.level > 0 ? (int64_t)A.ev[i].sample : A.base + i;
+    int64_t ls = A.level > 0 ? (int64_t)A.ev[i].sample : level0_local(A, i);
     path = A.level > 0 ? A.ev[i].path : 1u;
     if (A.rays0) {
         sample = (uint64_t)ls;
@@ -71,36 +76,48 @@ __device__ __forceinline__ void event_key(const LevelArgs& A, int64_t i, uint64_
     }
 }
 
-// wave-aggregated queue append: returns this lane's slot (valid only where `want`)
-__device__ __forceinline__ int32_t wave_append(unsigned int* counter, bool want) {
-    uint64_t mask = __ballot(want);
-    if (mask == 0) return -1;
-    const int lane = threadIdx.x & 63;
-    int leader = __ffsll((long long)mask) - 1;
-    unsigned int base = 0;
-    if (lane == leader) base = atomicAdd(counter, (unsigned int)__popcll(mask));
-    base = __shfl(base, leader, 64);
-    uint64_t below = lane == 0 ? 0ull : (mask & ((~0ull) >> (64 - lane)));
-    return (int32_t)(base + (unsigned int)__popcll(below));
+// Block-aggregated queue appends: the 4 waves' ballots are summed in LDS and one lane per queue
+// does a single device-scope atomicAdd for the whole block (device-scope atomics are performed
+// memory-side and serialise per address, so one per wave per queue was the kernels' bottleneck).
+// Every thread of the (256-thread) block must call it.  Returns this lane's slot where want[q].
+template <int NQ>
+__device__ __forceinline__ void block_append(unsigned int* const (&ctr)[NQ], const bool (&want)[NQ],
+                                             int32_t (&slot)[NQ]) {
+    __shared__ unsigned int s_cnt[NQ][4];
+    __shared__ unsigned int s_base[NQ][4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t m[NQ];
+    for (int q = 0; q < NQ; ++q) {
+        m[q] = __ballot(want[q]);
+        if (lane == 0) s_cnt[q][w] = (unsigned int)__popcll(m[q]);
+    }
+    __syncthreads();
+    if (threadIdx.x < NQ) {
+        const int q = threadIdx.x;
+        unsigned int total = s_cnt[q][0] + s_cnt[q][1] + s_cnt[q][2] + s_cnt[q][3];
+        unsigned int run = total ? atomicAdd(ctr[q], total) : 0u;
+        for (int k = 0; k < 4; ++k) {
+            s_base[q][k] = run;
+            run += s_cnt[q][k];
+        }
+    }
+    __syncthreads();
+    const uint64_t below_mask = lane == 0 ? 0ull : ((~0ull) >> (64 - lane));
+    for (int q = 0; q < NQ; ++q) slot[q] = (int32_t)(s_base[q][w] + (unsigned int)__popcll(m[q] & below_mask));
 }
 
-__device__ void flush(Counters& cnt, unsigned long long* counters) {
-    uint64_t s;
-    const bool l0 = (threadIdx.x & 63) == 0;
-    s = wave_sum_u64(cnt.rays);
-    if (l0 && s) atomicAdd(counters + C_RAYS, (unsigned long long)s);
-    s = wave_sum_u64(cnt.shadow);
-    if (l0 && s) atomicAdd(counters + C_SHADOW, (unsigned long long)s);
-    s = wave_sum_u64(cnt.shade);
-    if (l0 && s) atomicAdd(counters + C_SHADE, (unsigned long long)s);
-    s = wave_sum_u64(cnt.n1n2);
-    if (l0 && s) atomicAdd(counters + C_N1N2, (unsigned long long)s);
-    s = wave_sum_u64(cnt.gtests);
-    if (l0 && s) atomicAdd(counters + C_GROUP_TESTS, (unsigned long long)s);
-    s = wave_sum_u64(cnt.ghits);
-    if (l0 && s) atomicAdd(counters + C_GROUP_HITS, (unsigned long long)s);
-    s = wave_sum_u64(cnt.tests);
-    if (l0 && s) atomicAdd(counters + C_PRIM_TESTS, (unsigned long long)s);
+enum WalkKind { W_NONE = -1, W_TRACE = 0, W_SHADOW = 1, W_N1N2 = 2 };
+__device__ void flush(Counters& cnt, unsigned long long* counters, int walk = W_NONE) {
+    if ((threadIdx.x & 63) != 0) return;  // every field is wave-uniform
+    counters += (blockIdx.x & (RR_CNT_SLOTS - 1)) * RR_CNT_STRIDE;
+    const uint64_t v[7] = {cnt.rays, cnt.shadow, cnt.shade, cnt.n1n2, cnt.gtests, cnt.ghits, cnt.tests};
+    const int slot[7] = {C_RAYS, C_SHADOW, C_SHADE, C_N1N2, C_GROUP_TESTS, C_GROUP_HITS, C_PRIM_TESTS};
+    for (int k = 0; k < 7; ++k)
+        if (v[k]) atomicAdd(counters + slot[k], (unsigned long long)v[k]);
+    if (walk >= 0) {
+        if (cnt.flops) atomicAdd(counters + C_FLOPS_TRACE + walk, (unsigned long long)cnt.flops);
+        if (cnt.visits) atomicAdd(counters + C_VISITS_TRACE + walk, (unsigned long long)cnt.visits);
+    }
 }
 
 __device__ __forceinline__ bool needs_n1n2(const DevMaterial& m, int rem) {
@@ -109,16 +126,27 @@ __device__ __forceinline__ bool needs_n1n2(const DevMaterial& m, int rem) {
     return m.transparency != 0.0 && (rem > 0 || m.reflective > 0.0);
 }
 
-template <bool G>
+template <bool G, bool LC>
 __global__ void __launch_bounds__(256) trace_kernel(DevScene S, LevelArgs A) {
+    if (LC) stage_culls(S);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < A.n;
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0};
+    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef RR_STAMPS
+    cnt.st = nullptr;
+    if (A.stamps && A.level == 0) {
+        const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        cnt.st = A.stamps + (0 * (int64_t)(1 << 16) + w) * 8;
+        if (w >= (1 << 16)) cnt.st = nullptr;
+    }
+    RR_STAMP(cnt, 0);
+#endif
     Ray r = valid ? event_ray(A, i) : Ray{mk(0, 0, 0), mk(0, 0, 1)};
     Hit h;
-    trace_closest<G>(S, r, valid, h, cnt);
+    RR_STAMP(cnt, 1);
+    trace_closest<G, LC>(S, r, valid, h, cnt);
+    cnt.rays += popc_ballot(valid);
     if (valid) {
-        cnt.rays++;
         HitRec hr;
         hr.t = h.t;
         hr.u = h.u;
@@ -132,19 +160,30 @@ __global__ void __launch_bounds__(256) trace_kernel(DevScene S, LevelArgs A) {
         DevMaterial m = S.mats[S.nodes[h.node].material];
         want = needs_n1n2(m, A.rem);
     }
-    if (S.has_transparent) {
-        int32_t slot = wave_append(A.lcount + LC_N1N2, want);
-        if (want) A.n1n2_list[slot] = (int32_t)i;
+    if (S.has_transparent) {  // uniform: the whole block appends
+        unsigned int* const ctr[1] = {A.lcount + LC_N1N2};
+        const bool wq[1] = {want};
+        int32_t slot[1];
+        block_append<1>(ctr, wq, slot);
+        if (want) A.n1n2_list[slot[0]] = (int32_t)i;
     }
-    flush(cnt, A.counters);
+    RR_STAMP(cnt, 5);
+    flush(cnt, A.counters, W_TRACE);
+#ifdef RR_STAMPS
+    if (cnt.st && (threadIdx.x & 63) == 0) {
+        cnt.st[6] = cnt.visits;
+        cnt.st[7] = __builtin_amdgcn_s_memtime();
+    }
+#endif
 }
 
-template <bool G>
+template <bool G, bool LC>
 __global__ void __launch_bounds__(256) n1n2_kernel(DevScene S, LevelArgs A) {
+    if (LC) stage_culls(S);
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t cnt_n = (int64_t)A.lcount[LC_N1N2];
     const bool valid = j < cnt_n;
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0};
+    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int64_t i = valid ? A.n1n2_list[j] : 0;
     Ray r = valid ? event_ray(A, i) : Ray{mk(0, 0, 0), mk(0, 0, 1)};
     Hit h;
@@ -161,18 +200,18 @@ __global__ void __launch_bounds__(256) n1n2_kernel(DevScene S, LevelArgs A) {
         h.k = hr.k;
     }
     double n1 = 1.0, n2 = 1.0;
-    n1n2_walk<G>(S, r, h, valid, n1, n2, cnt);
+    n1n2_walk<G, LC>(S, r, h, valid, n1, n2, cnt);
     if (valid) {
         A.n12[2 * i] = n1;
         A.n12[2 * i + 1] = n2;
     }
-    flush(cnt, A.counters);
+    flush(cnt, A.counters, W_N1N2);
 }
 
 __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < A.n;
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0};
+    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     HitRec hr;
     hr.node = -1;
     if (valid) hr = A.hit[i];
@@ -196,8 +235,8 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
     Comps c;
     uint64_t sample = 0;
     uint32_t path = 1u;
+    cnt.shade += popc_ballot(has_hit);
     if (has_hit) {
-        cnt.shade++;
         Ray r = event_ray(A, i);
         Hit h;
         h.found = true;
@@ -254,7 +293,11 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
     }
     if (valid) A.comb[i] = cr;
     // children of this level -> next level queue (wave-aggregated appends keep siblings adjacent)
-    int32_t s1 = wave_append(A.lcount + LC_CHILDREN, do_refl);
+    unsigned int* const ctr[3] = {A.lcount + LC_CHILDREN, A.lcount + LC_CHILDREN, A.lcount + LC_LIT};
+    const bool wq[3] = {do_refl, do_refr, has_hit};
+    int32_t slots[3];
+    block_append<3>(ctr, wq, slots);
+    const int32_t s1 = slots[0], s2 = slots[1], sl = slots[2];
     if (do_refl) {
         Event e;
         e.o[0] = rr.o.x;
@@ -263,13 +306,12 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
         e.d[0] = rr.d.x;
         e.d[1] = rr.d.y;
         e.d[2] = rr.d.z;
-        e.sample = A.level > 0 ? A.ev[i].sample : (uint32_t)(A.base + i);
+        e.sample = A.level > 0 ? A.ev[i].sample : (uint32_t)level0_local(A, i);
         e.path = path * 2u;
         e.parent = (int32_t)i;
         e.slot = 0;
         A.next[s1] = e;
     }
-    int32_t s2 = wave_append(A.lcount + LC_CHILDREN, do_refr);
     if (do_refr) {
         Event e;
         e.o[0] = refr.o.x;
@@ -278,25 +320,34 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
         e.d[0] = refr.d.x;
         e.d[1] = refr.d.y;
         e.d[2] = refr.d.z;
-        e.sample = A.level > 0 ? A.ev[i].sample : (uint32_t)(A.base + i);
+        e.sample = A.level > 0 ? A.ev[i].sample : (uint32_t)level0_local(A, i);
         e.path = path * 2u + 1u;
         e.parent = (int32_t)i;
         e.slot = 1;
         A.next[s2] = e;
     }
-    int32_t sl = wave_append(A.lcount + LC_LIT, has_hit);
     if (has_hit) A.lit[sl] = (int32_t)i;
     flush(cnt, A.counters);
 }
 
 // one work-item per (lit hit, shadow slot j): j enumerates lights, and level^2 samples for area
 // lights (light.rs:47-65 sample_point with the deterministic jitter)
-template <bool G>
+template <bool G, bool LC>
 __global__ void __launch_bounds__(256) shadow_kernel(DevScene S, LevelArgs A) {
+    if (LC) stage_culls(S);
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t total = (int64_t)A.lcount[LC_LIT] * A.n_sr;
     const bool valid = idx < total;
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0};
+    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef RR_STAMPS
+    cnt.st = nullptr;
+    if (A.stamps && A.level == 0) {
+        const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        cnt.st = A.stamps + (1 * (int64_t)(1 << 16) + w) * 8;
+        if (w >= (1 << 16)) cnt.st = nullptr;
+    }
+    RR_STAMP(cnt, 0);
+#endif
     V3 p = mk(0, 0, 0), target = mk(0, 0, 1);
     if (valid) {
         int64_t L = idx / A.n_sr;
@@ -325,9 +376,17 @@ __global__ void __launch_bounds__(256) shadow_kernel(DevScene S, LevelArgs A) {
                           vmul(mk(Lt.v[0], Lt.v[1], Lt.v[2]), vf));
         }
     }
-    bool sh = shadowed<G>(S, p, target, valid, cnt);
+    RR_STAMP(cnt, 1);
+    bool sh = shadowed<G, LC>(S, p, target, valid, cnt);
     if (valid) A.sb[idx] = sh ? 1 : 0;
-    flush(cnt, A.counters);
+    RR_STAMP(cnt, 5);
+    flush(cnt, A.counters, W_SHADOW);
+#ifdef RR_STAMPS
+    if (cnt.st && (threadIdx.x & 63) == 0) {
+        cnt.st[6] = cnt.visits;
+        cnt.st[7] = __builtin_amdgcn_s_memtime();
+    }
+#endif
 }
 
 // shade_hit's light sum (scene.rs:159-166): surface = 0 + L0 + L1 + ...
@@ -380,7 +439,8 @@ __global__ void __launch_bounds__(256) combine_kernel(CombArgs C) {
     const CombRec c = C.comb[i];
     V3 v = (c.flags & CF_HIT) ? combine3(c) : mk(0.0, 0.0, 0.0);
     if (C.level == 0) {
-        double* o = C.out + 3 * (C.base + i);
+        const int64_t ls = C.lrows > 0 ? tile_to_local(C.base + i, C.hs, C.lrows) : C.base + i;
+        double* o = C.out + 3 * ls;
         o[0] = v.x;
         o[1] = v.y;
         o[2] = v.z;
@@ -422,25 +482,27 @@ __global__ void __launch_bounds__(256) aa_kernel(const double* __restrict__ canv
 }
 
 // Scene::is_shadowed for caller-given (point, light position) pairs
-template <bool G>
+template <bool G, bool LC>
 __global__ void __launch_bounds__(256) shadow_query_kernel(DevScene S, const double* __restrict__ pts,
                                                            const double* __restrict__ lps, int64_t n,
                                                            int32_t* __restrict__ out, unsigned long long* counters) {
+    if (LC) stage_culls(S);
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = i < n;
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0};
+    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     V3 p = mk(0, 0, 0), l = mk(0, 0, 1);
     if (valid) {
         p = mk(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]);
         l = mk(lps[3 * i], lps[3 * i + 1], lps[3 * i + 2]);
     }
-    bool sh = shadowed<G>(S, p, l, valid, cnt);
+    bool sh = shadowed<G, LC>(S, p, l, valid, cnt);
     if (valid) out[i] = sh ? 1 : 0;
-    flush(cnt, counters);
+    flush(cnt, counters, W_SHADOW);
 }
 
 // ------------------------------------------------------------------ host-side launchers
 static inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
+static inline size_t cull_lds(const DevScene& S) { return S.lds_culls ? (size_t)S.n_nodes * sizeof(DevCull) : 0; }
 
 hipEvent_t KernelProf::get() {
     if (used == pool.size()) {
@@ -473,16 +535,16 @@ struct Span {  // brackets one launch with events when profiling
 };
 }  // namespace
 
-template <bool G>
+template <bool G, bool LC>
 static void launch_level_t(const DevScene& S, const LevelArgs& A, int64_t n_sr_upper, hipStream_t st,
                            KernelProf* prof) {
     {
         Span s(prof, K_TRACE, st);
-        hipLaunchKernelGGL(trace_kernel<G>, dim3(blocks_for(A.n)), dim3(256), 0, st, S, A);
+        hipLaunchKernelGGL((trace_kernel<G, LC>), dim3(blocks_for(A.n)), dim3(256), cull_lds(S), st, S, A);
     }
     if (S.has_transparent) {
         Span s(prof, K_N1N2, st);
-        hipLaunchKernelGGL(n1n2_kernel<G>, dim3(blocks_for(A.n)), dim3(256), 0, st, S, A);
+        hipLaunchKernelGGL((n1n2_kernel<G, LC>), dim3(blocks_for(A.n)), dim3(256), cull_lds(S), st, S, A);
     }
     {
         Span s(prof, K_SHADE, st);
@@ -490,7 +552,7 @@ static void launch_level_t(const DevScene& S, const LevelArgs& A, int64_t n_sr_u
     }
     if (n_sr_upper > 0) {
         Span s(prof, K_SHADOW, st);
-        hipLaunchKernelGGL(shadow_kernel<G>, dim3(blocks_for(n_sr_upper)), dim3(256), 0, st, S, A);
+        hipLaunchKernelGGL((shadow_kernel<G, LC>), dim3(blocks_for(n_sr_upper)), dim3(256), cull_lds(S), st, S, A);
     }
     if (S.n_lights > 0) {
         Span s(prof, K_FINISH, st);
@@ -501,10 +563,17 @@ static void launch_level_t(const DevScene& S, const LevelArgs& A, int64_t n_sr_u
 hipError_t launch_level(const DevScene& S, const LevelArgs& A, int64_t n_sr_upper, hipStream_t st,
                         KernelProf* prof) {
     if (A.n <= 0) return hipSuccess;
-    if (S.has_groups)
-        launch_level_t<true>(S, A, n_sr_upper, st, prof);
-    else
-        launch_level_t<false>(S, A, n_sr_upper, st, prof);
+    if (S.has_groups) {
+        if (S.lds_culls)
+            launch_level_t<true, true>(S, A, n_sr_upper, st, prof);
+        else
+            launch_level_t<true, false>(S, A, n_sr_upper, st, prof);
+    } else {
+        if (S.lds_culls)
+            launch_level_t<false, true>(S, A, n_sr_upper, st, prof);
+        else
+            launch_level_t<false, false>(S, A, n_sr_upper, st, prof);
+    }
     return hipGetLastError();
 }
 
@@ -524,14 +593,27 @@ hipError_t launch_aa(const double* canvas, double* out, int64_t width, int64_t r
     return hipGetLastError();
 }
 
+template <bool G, bool LC>
+static void launch_shadow_query_t(const DevScene& S, const double* pts, const double* lps, int64_t n, int32_t* out,
+                                  unsigned long long* counters, hipStream_t st) {
+    hipLaunchKernelGGL((shadow_query_kernel<G, LC>), dim3(blocks_for(n)), dim3(256), cull_lds(S), st, S, pts, lps, n, out,
+                       counters);
+}
+
 hipError_t launch_shadow_query(const DevScene& S, const double* pts, const double* lps, int64_t n, int32_t* out,
                                unsigned long long* counters, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    if (S.has_groups)
-        hipLaunchKernelGGL(shadow_query_kernel<true>, dim3(blocks_for(n)), dim3(256), 0, st, S, pts, lps, n, out, counters);
-    else
-        hipLaunchKernelGGL(shadow_query_kernel<false>, dim3(blocks_for(n)), dim3(256), 0, st, S, pts, lps, n, out,
-                           counters);
+    if (S.has_groups) {
+        if (S.lds_culls)
+            launch_shadow_query_t<true, true>(S, pts, lps, n, out, counters, st);
+        else
+            launch_shadow_query_t<true, false>(S, pts, lps, n, out, counters, st);
+    } else {
+        if (S.lds_culls)
+            launch_shadow_query_t<false, true>(S, pts, lps, n, out, counters, st);
+        else
+            launch_shadow_query_t<false, false>(S, pts, lps, n, out, counters, st);
+    }
     return hipGetLastError();
 }
 

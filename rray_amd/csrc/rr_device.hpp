@@ -73,7 +73,17 @@ struct DevCamera {
     double inv[16];  // full 4x4 inverse of the camera transform (camera.rs:85)
 };
 
+// Conservative bounding sphere of a node's content in WORLD space (so any run of consecutive nodes,
+// at any group depth, can be tested against one world-space ray bundle): f32 centre + radius,
+// inflated so that every ray the exact f64 test can report as intersecting passes the f32 cull
+// (DESIGN.md §3.5).  radius = +inf: never culled (planes, unbounded groups).
+struct alignas(16) DevCull {
+    float c[3];
+    float r;
+};
+
 struct DevScene {
+    const DevCull* culls;
     const DevNode* nodes;
     const DevGroup* groups;
     const DevTri* tris;
@@ -83,7 +93,11 @@ struct DevScene {
     int32_t n_nodes, n_lights;
     int32_t has_transparent;  // any material with transparency != 0 (enables the n1/n2 walk)
     int32_t has_groups;
+    int32_t lds_culls;        // culls staged in LDS per workgroup (n_nodes <= RR_LDS_CULL_CAP)
+    int32_t pad;
 };
+// Up to this many cull records (16 B each) are copied into LDS by every walking workgroup.
+constexpr int RR_LDS_CULL_CAP = 2048;
 
 // Per-launch counters (u64, zeroed by the host before each launch).
 enum Counter {
@@ -96,7 +110,18 @@ enum Counter {
     C_SAMPLES,
     C_PRIM_TESTS,
     C_WORK,  // work-queue head
+    C_FLOPS_TRACE,   // f64 flops of the exact tests executed (SURVEY §8d model), per walk kind
+    C_FLOPS_SHADOW,
+    C_FLOPS_N1N2,
+    C_VISITS_TRACE,  // node visits x 64 (one per lane of a wave that ran a candidate's exact test)
+    C_VISITS_SHADOW,
+    C_VISITS_N1N2,
     C_COUNT
 };
+// Counters live in RR_CNT_SLOTS copies (slot = blockIdx % RR_CNT_SLOTS, RR_CNT_STRIDE u64 each) so
+// that concurrent workgroups' device-scope atomics hit different addresses; the host sums them.
+constexpr int RR_CNT_SLOTS = 256;
+constexpr int RR_CNT_STRIDE = 16;
+static_assert(C_COUNT <= RR_CNT_STRIDE, "counter slot layout");
 
 }  // namespace rr

@@ -21,5 +21,6 @@ run() {  # name, timeout, rocprof args...
 run kt 300 --kernel-trace --stats || exit 1
 run pmc_fetch 300 --pmc FETCH_SIZE || exit 1
 run pmc_write 300 --pmc WRITE_SIZE || exit 1
-run pmc_sq 300 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES || exit 1
+run pmc_sq 300 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU || exit 1
+run pmc_sq2 300 --pmc SQ_WAVES SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH GRBM_GUI_ACTIVE
 find "$OUT" -name "*.csv" | head -50

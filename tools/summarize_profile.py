@@ -36,6 +36,8 @@ def main(src, tag, workload="c2_s1024"):
     fetch = per_kernel(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
     write = per_kernel(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
     sq = per_kernel(os.path.join(src, "pmc_sq", "run_counter_collection.csv"))
+    sq2_path = os.path.join(src, "pmc_sq2", "run_counter_collection.csv")
+    sq2 = per_kernel(sq2_path) if os.path.exists(sq2_path) else {}
     out = {"workload": workload, "source": "rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE | WRITE_SIZE | "
            "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES (separate passes)", "kernels": {}}
     for r in stats:
@@ -44,18 +46,24 @@ def main(src, tag, workload="c2_s1024"):
             continue
         f = fetch.get(r["Name"], {}).get("FETCH_SIZE")
         w = write.get(r["Name"], {}).get("WRITE_SIZE")
-        s = sq.get(r["Name"], {})
+        s = dict(sq2.get(r["Name"], {}))
+        s.update(sq.get(r["Name"], {}))
         hbm = None if f is None or w is None else (2 * f + w) * 1024
         out["kernels"][k] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                              "pct": float(r["Percentage"]), "fetch_kib_raw": f, "write_kib": w,
                              "hbm_bytes_per_launch": hbm,
-                             "valu_insts_per_wave": (s["SQ_INSTS_VALU"] / s["SQ_WAVES"]) if s.get("SQ_WAVES") else None}
+                             "valu_insts_per_wave": (s["SQ_INSTS_VALU"] / s["SQ_WAVES"]) if s.get("SQ_WAVES") else None,
+                             # per-wave averages of every SQ counter (SQ_WAVE_CYCLES / WAIT / ACTIVE in quad-cycles)
+                             "sq_per_wave": {c: v / s["SQ_WAVES"] for c, v in s.items()
+                                             if c.startswith("SQ_") and c != "SQ_WAVES"} if s.get("SQ_WAVES") else None,
+                             "sq_waves": s.get("SQ_WAVES"), "grbm_gui_active": s.get("GRBM_GUI_ACTIVE")}
     json.dump(out, open(f"profiles/{tag}_summary.json", "w"), indent=1)
     json.dump({k: {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"]} for k, v in out["kernels"].items()},
               open(f"profiles/pmc_{workload}.json", "w"), indent=1)
     shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), f"profiles/{tag}_kernel_stats.csv")
-    for p in ("pmc_fetch", "pmc_write", "pmc_sq"):
-        shutil.copy(os.path.join(src, p, "run_counter_collection.csv"), f"profiles/{tag}_{p}.csv")
+    for p in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2"):
+        if os.path.exists(os.path.join(src, p, "run_counter_collection.csv")):
+            shutil.copy(os.path.join(src, p, "run_counter_collection.csv"), f"profiles/{tag}_{p}.csv")
     print(json.dumps(out, indent=1))
 
 
