@@ -113,11 +113,16 @@ def main():
     # roofline of the dominant kernel (rank 0's measurements)
     dom = max(ktimes, key=lambda k: ktimes[k][0])
     dom_ms, dom_n = ktimes[dom]
-    walk = {"trace": 0, "shadow": 1, "n1n2": 2}
-    if dom in walk:  # f64 flops of the exact tests this kernel executed after culling (last step)
-        flops = stats["exact_flops"][walk[dom]]
+    # f64 flops this kernel executed in the last step: the exact leaf tests its walks ran after culling
+    # (trace / n1n2 walks; the shade kernel runs the is_shadowed walks) + the shade-event model
+    if dom == "trace":
+        flops = stats["exact_flops"][0]
+    elif dom == "n1n2":
+        flops = stats["exact_flops"][2]
+    elif dom == "shade":
+        flops = stats["exact_flops"][1] + stats["shade_events"] * FLOPS["shade"]
     else:
-        flops = stats["shade_events"] * FLOPS["shade"]
+        flops = 0
     launches_per_frame = dom_n / args.steps
     # flops of one step / (this kernel's time per step) == per-launch flops / average launch duration
     achieved = flops / (dom_ms / args.steps / 1e3) / 1e12 if dom_ms > 0 else 0.0
@@ -132,9 +137,9 @@ def main():
                 "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": traffic, "kernel": dom,
                 "kernel_ms": round(dom_ms / dom_n, 4), "launches_per_step": launches_per_frame,
                 "flops_per_launch": flops / launches_per_frame,
-                "note": "achieved = f64 flops of the exact leaf tests the kernel executed (SURVEY §8d model: "
-                        "sphere 57, plane 13, triangle/group 45) / kernel time; the f32 bundle/line culling that "
-                        "removes the other tests is overhead, not counted. Peak = MI355X FP64 vector = FP64 MFMA "
+                "note": "achieved = f64 flops the kernel executed: exact leaf tests after culling (SURVEY §8d model: "
+                        "sphere 57, plane 13, triangle/group 45) + 250 per shade event for the shade kernel, / kernel "
+                        "time; the f32 bundle/line culling that removes the other tests is overhead, not counted. Peak = MI355X FP64 vector = FP64 MFMA "
                         "dense 78.6 TF; bit-parity forbids FMA contraction (DESIGN.md §4)"}
 
     cpu = None

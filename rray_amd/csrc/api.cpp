@@ -64,11 +64,10 @@ struct rr_ctx {
     bool has_scene = false;
     rr::HostScene host;
     rr::DevScene S{};
-    DBuf culls, nodes, groups, tris, mats, pats, lights, sr_light, sr_s;
-    int32_t n_sr = 0;
+    DBuf culls, nodes, groups, tris, mats, pats, lights;
     // workspace
-    DBuf counters, lcount, hit, n12, sr, lit, sb, n1n2, ev_a, ev_b, canvas, rays0, qout;
-    std::vector<DBuf> comb;  // one per level
+    DBuf counters, lcount, hit, n12, n1n2, ev_a, ev_b, canvas, rays0, qout;
+    std::vector<DBuf> comb, pend;  // one per level
     unsigned int* h_lcount = nullptr;  // pinned
     unsigned long long* h_counters = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -137,15 +136,16 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
         int64_t n = nb;
         DBuf* cur_ev = nullptr;
         DBuf* nxt_ev = &c->ev_a;
+        std::vector<int64_t> level_pend;
         for (int d = 0; d <= max_depth && n > 0; ++d) {
-            if ((int)c->comb.size() <= d) c->comb.resize(d + 1);
-            const int64_t nsr = std::max<int64_t>(c->n_sr, 1);
+            if ((int)c->comb.size() <= d) {
+                c->comb.resize(d + 1);
+                c->pend.resize(d + 1);
+            }
             HIPCHK(c->hit.ensure(n * sizeof(rr::HitRec)));
             HIPCHK(c->n12.ensure(n * 2 * sizeof(double)));
-            HIPCHK(c->sr.ensure(n * sizeof(rr::ShadeRec)));
             HIPCHK(c->comb[d].ensure(n * sizeof(rr::CombRec)));
-            HIPCHK(c->lit.ensure(n * sizeof(int32_t)));
-            HIPCHK(c->sb.ensure(n * nsr));
+            HIPCHK(c->pend[d].ensure(n * sizeof(int32_t)));
             HIPCHK(c->n1n2.ensure(n * sizeof(int32_t)));
             const bool children_possible = d < max_depth;
             if (children_possible) HIPCHK(nxt_ev->ensure(2 * n * sizeof(rr::Event)));
@@ -158,16 +158,13 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             A.ev = cur_ev ? cur_ev->as<rr::Event>() : nullptr;
             A.hit = c->hit.as<rr::HitRec>();
             A.n12 = c->n12.as<double>();
-            A.sr = c->sr.as<rr::ShadeRec>();
             A.comb = c->comb[d].as<rr::CombRec>();
+            A.parent_comb = d > 0 ? c->comb[d - 1].as<rr::CombRec>() : nullptr;
+            A.out = out;
             A.next = children_possible ? nxt_ev->as<rr::Event>() : nullptr;
-            A.lit = c->lit.as<int32_t>();
-            A.sb = c->sb.as<uint8_t>();
+            A.pending = c->pend[d].as<int32_t>();
             A.n1n2_list = c->n1n2.as<int32_t>();
             A.lcount = c->lcount.as<unsigned int>();
-            A.n_sr = c->n_sr;
-            A.sr_light = c->sr_light.as<int32_t>();
-            A.sr_s = c->sr_s.as<int32_t>();
             A.counters = c->counters.as<unsigned long long>();
             A.stamps = nullptr;
 #ifdef RR_STAMPS
@@ -182,7 +179,7 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
                 A.stamps = stamp_buf.as<unsigned long long>();
             }
 #endif
-            HIPCHK(rr::launch_level(c->S, A, n * (int64_t)c->n_sr, st, c->profile ? &c->prof : nullptr));
+            HIPCHK(rr::launch_level(c->S, A, st, c->profile ? &c->prof : nullptr));
 #ifdef RR_STAMPS
             if (A.stamps) {
                 std::vector<unsigned long long> hv(stamp_bytes / sizeof(unsigned long long));
@@ -195,20 +192,26 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             }
 #endif
             level_n.push_back(n);
-            if (!children_possible) break;
+            if (!children_possible) {  // no children at the last level, so nothing is pending
+                level_pend.push_back(0);
+                break;
+            }
             HIPCHK(hipMemcpyAsync(c->h_lcount, c->lcount.p, rr::LC_COUNT * sizeof(unsigned int), hipMemcpyDeviceToHost,
                                   st));
             HIPCHK(hipStreamSynchronize(st));
+            level_pend.push_back((int64_t)c->h_lcount[rr::LC_PENDING]);
             n = (int64_t)c->h_lcount[rr::LC_CHILDREN];
             cur_ev = nxt_ev;
             nxt_ev = (nxt_ev == &c->ev_a) ? &c->ev_b : &c->ev_a;
         }
-        // bottom-up shade_hit sums (scene.rs:172-177); level 0 writes the results
+        // bottom-up shade_hit sums of the events with children (scene.rs:172-177)
         for (int d = (int)level_n.size() - 1; d >= 0; --d) {
+            if (level_pend[d] == 0) continue;
             rr::CombArgs C{};
             C.level = d;
-            C.n = level_n[d];
+            C.n = level_pend[d];
             C.base = base;
+            C.pending = c->pend[d].as<int32_t>();
             C.comb = c->comb[d].as<rr::CombRec>();
             C.parent_comb = d > 0 ? c->comb[d - 1].as<rr::CombRec>() : nullptr;
             C.out = out;
@@ -312,11 +315,11 @@ void rr_destroy(rr_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (DBuf* b : {&c->culls, &c->nodes, &c->groups, &c->tris, &c->mats, &c->pats, &c->lights, &c->sr_light, &c->sr_s,
-                    &c->counters, &c->lcount, &c->hit, &c->n12, &c->sr, &c->lit, &c->sb, &c->n1n2, &c->ev_a, &c->ev_b,
-                    &c->canvas, &c->rays0, &c->qout})
+    for (DBuf* b : {&c->culls, &c->nodes, &c->groups, &c->tris, &c->mats, &c->pats, &c->lights, &c->counters,
+                    &c->lcount, &c->hit, &c->n12, &c->n1n2, &c->ev_a, &c->ev_b, &c->canvas, &c->rays0, &c->qout})
         b->release();
     for (auto& b : c->comb) b.release();
+    for (auto& b : c->pend) b.release();
     for (hipEvent_t e : c->prof.pool) (void)hipEventDestroy(e);
     if (c->h_lcount) (void)hipHostFree(c->h_lcount);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
@@ -341,20 +344,7 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     HIPCHK(upload(c->mats, hs.mats, st));
     HIPCHK(upload(c->pats, hs.pats, st));
     HIPCHK(upload(c->lights, hs.lights, st));
-    // shadow slots: one per point light, level^2 per area light (scene.rs:181-214)
-    std::vector<int32_t> sl, ss;
-    for (size_t li = 0; li < hs.lights.size(); ++li) {
-        const rr::DevLight& L = hs.lights[li];
-        int amount = L.kind == RR_LIGHT_POINT ? 1 : L.level * L.level;
-        for (int s = 0; s < amount; ++s) {
-            sl.push_back((int32_t)li);
-            ss.push_back(s);
-        }
-    }
-    HIPCHK(upload(c->sr_light, sl, st));
-    HIPCHK(upload(c->sr_s, ss, st));
     HIPCHK(hipStreamSynchronize(st));
-    c->n_sr = (int32_t)sl.size();
     c->host = std::move(hs);
     rr::DevScene& S = c->S;
     S.culls = c->culls.as<rr::DevCull>();

@@ -23,16 +23,13 @@ struct LevelArgs {
     const Event* ev;         // level >= 1 input queue
     HitRec* hit;
     double* n12;
-    ShadeRec* sr;
-    CombRec* comb;
+    CombRec* comb;           // this level's pending sums (indexed by event)
+    CombRec* parent_comb;    // level - 1 (children deliver into their parent's slot)
+    double* out;             // level 0: canvas / color_at results (3 doubles per local sample)
     Event* next;
-    int32_t* lit;
-    uint8_t* sb;
+    int32_t* pending;        // this level's events with children
     int32_t* n1n2_list;
     unsigned int* lcount;    // LC_* (zeroed per level)
-    int32_t n_sr;            // shadow slots per lit hit
-    const int32_t* sr_light;
-    const int32_t* sr_s;
     uint64_t seed;
     int32_t jitter_mode;
     unsigned long long* counters;  // C_* totals
@@ -41,8 +38,9 @@ struct LevelArgs {
 
 struct CombArgs {
     int32_t level;
-    int64_t n;
+    int64_t n;                 // pending events of this level
     int64_t base;
+    const int32_t* pending;
     const CombRec* comb;
     CombRec* parent_comb;
     double* out;  // level 0: canvas (3 doubles per local sample)
@@ -76,8 +74,7 @@ struct KernelProf {
     hipEvent_t get();
 };
 
-hipError_t launch_level(const DevScene& S, const LevelArgs& A, int64_t n_sr_upper, hipStream_t stream,
-                        KernelProf* prof = nullptr);
+hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t stream, KernelProf* prof = nullptr);
 hipError_t launch_combine(const CombArgs& C, hipStream_t stream, KernelProf* prof = nullptr);
 hipError_t launch_aa(const double* canvas, double* out, int64_t width, int64_t rows, int32_t aa, hipStream_t stream,
                      KernelProf* prof = nullptr);

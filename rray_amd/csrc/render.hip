@@ -4,13 +4,12 @@
 // level over HBM-resident queues (wavefront.hpp):
 //   trace_kernel   closest hit per pending color_at ray           scene.rs:97-106,130
 //   n1n2_kernel    container walk for transparent hits             intersection.rs:61-92
-//   shade_kernel   prepare_computations, pattern, children rays    intersection.rs:50-60, scene.rs:281-336
-//   shadow_kernel  is_shadowed for every (hit, light, sample)      scene.rs:181-214,234-245
-//   finish_kernel  lighting sum per hit                            scene.rs:159-166, light.rs:98-140
-//   combine_kernel bottom-up shade_hit sums                        scene.rs:167-177
+//   shade_kernel   prepare_computations, pattern, children rays,   intersection.rs:50-60, scene.rs:159-336,
+//                  is_shadowed walks + lighting sum, leaf results  light.rs:47-140
+//   combine_kernel bottom-up shade_hit sums of events with children scene.rs:167-177
 //   aa_kernel      box average before `as u8`                      canvas.rs:76-96
-// Every kernel is one work-item per queue entry; the node loops inside are wave-uniform (scalar
-// broadcast loads of the flattened scene) so the f64 VALU does all the work.
+// Every kernel is one work-item per queue entry; the node walks inside are wave-uniform (scalar
+// broadcast loads of the flattened scene, culled per wave against the rays' bundle).
 #include "device_core.inc"
 #include "kernels.hpp"
 #include "wavefront.hpp"
@@ -208,7 +207,49 @@ __global__ void __launch_bounds__(256) n1n2_kernel(DevScene S, LevelArgs A) {
     flush(cnt, A.counters, W_N1N2);
 }
 
+// shade_hit's final sum (scene.rs:172-177) for given child results a (reflected) and b (refracted)
+__device__ __forceinline__ V3 shade_sum(V3 s, V3 a, V3 b, double refl, double transp, double R) {
+    if (refl > 0.0 && transp > 0.0) return vadd(vadd(s, vmul(a, R)), vmul(b, 1.0 - R));
+    return vadd(vadd(s, a), b);
+}
+
+// A finished color_at value v of event i: level 0 writes the canvas; deeper levels become the
+// parent's reflected_color (v * reflective, scene.rs:281-290) or refracted_color (v * transparency,
+// scene.rs:310-336) slot.  Each slot has exactly one writer.
+__device__ __forceinline__ void deliver(int32_t level, int64_t i, int32_t parent, int32_t slot, V3 v, double* out,
+                                        CombRec* parent_comb, int64_t out_index) {
+    if (level == 0) {
+        double* o = out + 3 * out_index;
+        o[0] = v.x;
+        o[1] = v.y;
+        o[2] = v.z;
+        return;
+    }
+    CombRec& p = parent_comb[parent];
+    if (slot) {
+        const double t = p.transp;
+        p.refr_res[0] = v.x * t;
+        p.refr_res[1] = v.y * t;
+        p.refr_res[2] = v.z * t;
+    } else {
+        const double t = p.refl;
+        p.refl_res[0] = v.x * t;
+        p.refl_res[1] = v.y * t;
+        p.refl_res[2] = v.z * t;
+    }
+}
+
+// Fused shade_hit for every event of the level (scene.rs:159-177):
+//   prepare_computations + pattern (intersection.rs:50-60, material.rs:77-80), the children rays
+//   (reflected_color scene.rs:281-290, refracted_color scene.rs:310-336) appended to level d+1,
+//   then surface = 0 + lighting(L0, intensity_at(L0)) + ... with every is_shadowed walk
+//   (scene.rs:181-214, 234-245; area lights sample level^2 jittered points, light.rs:47-65).
+// The 64 lanes of a wave walk their shadow rays for the same light sample together, so the walk's
+// ray bundle stays tight.  Events without children are finished here (deliver); events with
+// children store their pending sum and are finished by combine_kernel after their children.
+template <bool G, bool LC>
 __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
+    if (LC) stage_culls(S);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < A.n;
     Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -221,21 +262,14 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
         parent = A.ev[i].parent;
         slot = A.ev[i].slot;
     }
-    CombRec cr;
-    cr.surf[0] = cr.surf[1] = cr.surf[2] = 0.0;
-    cr.refl_res[0] = cr.refl_res[1] = cr.refl_res[2] = 0.0;
-    cr.refr_res[0] = cr.refr_res[1] = cr.refr_res[2] = 0.0;
-    cr.refl = 0.0;
-    cr.transp = 0.0;
-    cr.R = 0.0;
-    cr.parent = parent;
-    cr.flags = slot ? CF_REFRACT_CHILD : 0;
+    cnt.shade += popc_ballot(has_hit);
+    V3 over = mk(0, 0, 0), eyev = mk(0, 0, 1), normalv = mk(0, 0, 1), pcol = mk(0, 0, 0);
+    int32_t mat = 0;
+    double refl = 0.0, transp = 0.0, R = 0.0;
     bool do_refl = false, do_refr = false;
-    Ray rr, refr;
-    Comps c;
+    Ray rr = {mk(0, 0, 0), mk(0, 0, 1)}, refr = rr;
     uint64_t sample = 0;
     uint32_t path = 1u;
-    cnt.shade += popc_ballot(has_hit);
     if (has_hit) {
         Ray r = event_ray(A, i);
         Hit h;
@@ -245,30 +279,18 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
         h.v = hr.v;
         h.node = hr.node;
         h.k = hr.k;
+        Comps c;
         prepare(S, r, h, c);  // intersection.rs:50-60
-        DevMaterial m = S.mats[S.nodes[hr.node].material];
+        mat = S.nodes[hr.node].material;
+        const DevMaterial m = S.mats[mat];
         if (S.has_transparent && needs_n1n2(m, A.rem)) {
             c.n1 = A.n12[2 * i];
             c.n2 = A.n12[2 * i + 1];
         }
-        V3 pcol = pattern_at(S, m.pattern, world_to_object(S, hr.node, c.over));  // material.rs:77-80
-        ShadeRec sr;
-        sr.over[0] = c.over.x;
-        sr.over[1] = c.over.y;
-        sr.over[2] = c.over.z;
-        sr.eyev[0] = c.eyev.x;
-        sr.eyev[1] = c.eyev.y;
-        sr.eyev[2] = c.eyev.z;
-        sr.normalv[0] = c.normalv.x;
-        sr.normalv[1] = c.normalv.y;
-        sr.normalv[2] = c.normalv.z;
-        sr.pcol[0] = pcol.x;
-        sr.pcol[1] = pcol.y;
-        sr.pcol[2] = pcol.z;
-        sr.material = S.nodes[hr.node].material;
-        sr.pad = 0;
-        A.sr[i] = sr;
-        // reflected_color (scene.rs:281-290) / refracted_color (scene.rs:310-336)
+        pcol = pattern_at(S, m.pattern, world_to_object(S, hr.node, c.over));  // material.rs:77-80
+        over = c.over;
+        eyev = c.eyev;
+        normalv = c.normalv;
         do_refl = A.rem > 0 && m.reflective != 0.0;
         if (do_refl) {
             rr.o = c.over;
@@ -285,179 +307,110 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
                 do_refr = true;
             }
         }
-        cr.refl = m.reflective;
-        cr.transp = m.transparency;
-        cr.R = (m.reflective > 0.0 && m.transparency > 0.0) ? schlick(c) : 0.0;
-        cr.flags |= CF_HIT;
-        if (do_refl || do_refr) event_key(A, i, sample, path);
+        refl = m.reflective;
+        transp = m.transparency;
+        R = (m.reflective > 0.0 && m.transparency > 0.0) ? schlick(c) : 0.0;
+        event_key(A, i, sample, path);
     }
-    if (valid) A.comb[i] = cr;
-    // children of this level -> next level queue (wave-aggregated appends keep siblings adjacent)
-    unsigned int* const ctr[3] = {A.lcount + LC_CHILDREN, A.lcount + LC_CHILDREN, A.lcount + LC_LIT};
-    const bool wq[3] = {do_refl, do_refr, has_hit};
-    int32_t slots[3];
-    block_append<3>(ctr, wq, slots);
-    const int32_t s1 = slots[0], s2 = slots[1], sl = slots[2];
-    if (do_refl) {
-        Event e;
-        e.o[0] = rr.o.x;
-        e.o[1] = rr.o.y;
-        e.o[2] = rr.o.z;
-        e.d[0] = rr.d.x;
-        e.d[1] = rr.d.y;
-        e.d[2] = rr.d.z;
-        e.sample = A.level > 0 ? A.ev[i].sample : (uint32_t)level0_local(A, i);
-        e.path = path * 2u;
-        e.parent = (int32_t)i;
-        e.slot = 0;
-        A.next[s1] = e;
-    }
-    if (do_refr) {
-        Event e;
-        e.o[0] = refr.o.x;
-        e.o[1] = refr.o.y;
-        e.o[2] = refr.o.z;
-        e.d[0] = refr.d.x;
-        e.d[1] = refr.d.y;
-        e.d[2] = refr.d.z;
-        e.sample = A.level > 0 ? A.ev[i].sample : (uint32_t)level0_local(A, i);
-        e.path = path * 2u + 1u;
-        e.parent = (int32_t)i;
-        e.slot = 1;
-        A.next[s2] = e;
-    }
-    if (has_hit) A.lit[sl] = (int32_t)i;
-    flush(cnt, A.counters);
-}
-
-// one work-item per (lit hit, shadow slot j): j enumerates lights, and level^2 samples for area
-// lights (light.rs:47-65 sample_point with the deterministic jitter)
-template <bool G, bool LC>
-__global__ void __launch_bounds__(256) shadow_kernel(DevScene S, LevelArgs A) {
-    if (LC) stage_culls(S);
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)A.lcount[LC_LIT] * A.n_sr;
-    const bool valid = idx < total;
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-#ifdef RR_STAMPS
-    cnt.st = nullptr;
-    if (A.stamps && A.level == 0) {
-        const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-        cnt.st = A.stamps + (1 * (int64_t)(1 << 16) + w) * 8;
-        if (w >= (1 << 16)) cnt.st = nullptr;
-    }
-    RR_STAMP(cnt, 0);
-#endif
-    V3 p = mk(0, 0, 0), target = mk(0, 0, 1);
-    if (valid) {
-        int64_t L = idx / A.n_sr;
-        int32_t j = (int32_t)(idx - L * A.n_sr);
-        int64_t e = A.lit[L];
-        const ShadeRec& sr = A.sr[e];
-        p = mk(sr.over[0], sr.over[1], sr.over[2]);
-        int li = A.sr_light[j];
-        DevLight Lt = S.lights[li];
-        if (Lt.kind == RR_LIGHT_POINT) {
-            target = mk(Lt.position[0], Lt.position[1], Lt.position[2]);
-        } else {
-            int s = A.sr_s[j];
-            int row = s / Lt.level, col = s % Lt.level;
-            double ur = 0.5, vr = 0.5;
-            if (A.jitter_mode == 0) {
-                uint64_t sample;
-                uint32_t path;
-                event_key(A, e, sample, path);
-                ur = jitter(A.seed, sample, path, (uint32_t)li, (uint32_t)s, 0);
-                vr = jitter(A.seed, sample, path, (uint32_t)li, (uint32_t)s, 1);
-            }
-            double uf = ((double)col + ur) / (double)Lt.level;
-            double vf = ((double)row + vr) / (double)Lt.level;
-            target = vadd(vadd(mk(Lt.corner[0], Lt.corner[1], Lt.corner[2]), vmul(mk(Lt.u[0], Lt.u[1], Lt.u[2]), uf)),
-                          vmul(mk(Lt.v[0], Lt.v[1], Lt.v[2]), vf));
+    // children of this level -> next level queue; parents -> this level's pending list
+    const bool pending = do_refl || do_refr;
+    {
+        unsigned int* const ctr[3] = {A.lcount + LC_CHILDREN, A.lcount + LC_CHILDREN, A.lcount + LC_PENDING};
+        const bool wq[3] = {do_refl, do_refr, pending};
+        int32_t slots[3];
+        block_append<3>(ctr, wq, slots);
+        const uint32_t ls = A.level > 0 ? A.ev[valid ? i : 0].sample : (uint32_t)level0_local(A, i);
+        if (do_refl) {
+            Event e;
+            e.o[0] = rr.o.x;
+            e.o[1] = rr.o.y;
+            e.o[2] = rr.o.z;
+            e.d[0] = rr.d.x;
+            e.d[1] = rr.d.y;
+            e.d[2] = rr.d.z;
+            e.sample = ls;
+            e.path = path * 2u;
+            e.parent = (int32_t)i;
+            e.slot = 0;
+            A.next[slots[0]] = e;
         }
+        if (do_refr) {
+            Event e;
+            e.o[0] = refr.o.x;
+            e.o[1] = refr.o.y;
+            e.o[2] = refr.o.z;
+            e.d[0] = refr.d.x;
+            e.d[1] = refr.d.y;
+            e.d[2] = refr.d.z;
+            e.sample = ls;
+            e.path = path * 2u + 1u;
+            e.parent = (int32_t)i;
+            e.slot = 1;
+            A.next[slots[1]] = e;
+        }
+        if (pending) A.pending[slots[2]] = (int32_t)i;
     }
-    RR_STAMP(cnt, 1);
-    bool sh = shadowed<G, LC>(S, p, target, valid, cnt);
-    if (valid) A.sb[idx] = sh ? 1 : 0;
-    RR_STAMP(cnt, 5);
-    flush(cnt, A.counters, W_SHADOW);
-#ifdef RR_STAMPS
-    if (cnt.st && (threadIdx.x & 63) == 0) {
-        cnt.st[6] = cnt.visits;
-        cnt.st[7] = __builtin_amdgcn_s_memtime();
-    }
-#endif
-}
-
-// shade_hit's light sum (scene.rs:159-166): surface = 0 + L0 + L1 + ...
-__global__ void __launch_bounds__(256) finish_kernel(DevScene S, LevelArgs A) {
-    const int64_t L = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (L >= (int64_t)A.lcount[LC_LIT]) return;
-    const int64_t e = A.lit[L];
-    const ShadeRec sr = A.sr[e];
-    const DevMaterial m = S.mats[sr.material];
-    V3 over = mk(sr.over[0], sr.over[1], sr.over[2]);
-    V3 eyev = mk(sr.eyev[0], sr.eyev[1], sr.eyev[2]);
-    V3 nrm = mk(sr.normalv[0], sr.normalv[1], sr.normalv[2]);
-    V3 pcol = mk(sr.pcol[0], sr.pcol[1], sr.pcol[2]);
+    // surface = 0 + L0 + L1 + ... (scene.rs:159-166)
     V3 surface = mk(0, 0, 0);
-    const uint8_t* bits = A.sb + L * A.n_sr;
-    int j = 0;
+    const DevMaterial m = S.mats[mat];
     for (int li = 0; li < S.n_lights; ++li) {
-        DevLight Lt = ldc(S.lights, li);
+        const DevLight Lt = ldc(S.lights, li);
         double in_shadow;
         if (Lt.kind == RR_LIGHT_POINT) {
-            in_shadow = bits[j] ? 1.0 : 0.0;
-            j += 1;
-        } else {
-            int amount = Lt.level * Lt.level, total = 0;
-            for (int s = 0; s < amount; ++s) total += bits[j + s];
+            const bool sh = shadowed<G, LC>(S, over, mk(Lt.position[0], Lt.position[1], Lt.position[2]), has_hit, cnt);
+            in_shadow = sh ? 1.0 : 0.0;
+        } else {  // light.rs:47-65: level^2 jittered cell samples
+            const int amount = Lt.level * Lt.level;
+            int total = 0;
+            for (int s = 0; s < amount; ++s) {
+                const int row = s / Lt.level, col = s % Lt.level;
+                double ur = 0.5, vr = 0.5;
+                if (A.jitter_mode == 0) {
+                    ur = jitter(A.seed, sample, path, (uint32_t)li, (uint32_t)s, 0);
+                    vr = jitter(A.seed, sample, path, (uint32_t)li, (uint32_t)s, 1);
+                }
+                const double uf = ((double)col + ur) / (double)Lt.level;
+                const double vf = ((double)row + vr) / (double)Lt.level;
+                const V3 target = vadd(vadd(mk(Lt.corner[0], Lt.corner[1], Lt.corner[2]),
+                                            vmul(mk(Lt.u[0], Lt.u[1], Lt.u[2]), uf)),
+                                       vmul(mk(Lt.v[0], Lt.v[1], Lt.v[2]), vf));
+                total += shadowed<G, LC>(S, over, target, has_hit, cnt) ? 1 : 0;
+            }
             in_shadow = (double)total / (double)amount;
-            j += amount;
         }
-        surface = vadd(surface, lighting(m, Lt, pcol, over, eyev, nrm, in_shadow));
+        if (has_hit) surface = vadd(surface, lighting(m, Lt, pcol, over, eyev, normalv, in_shadow));
     }
-    CombRec& cr = A.comb[e];
-    cr.surf[0] = surface.x;
-    cr.surf[1] = surface.y;
-    cr.surf[2] = surface.z;
+    if (pending) {
+        CombRec cr;
+        cr.surf[0] = surface.x;
+        cr.surf[1] = surface.y;
+        cr.surf[2] = surface.z;
+        cr.refl_res[0] = cr.refl_res[1] = cr.refl_res[2] = 0.0;
+        cr.refr_res[0] = cr.refr_res[1] = cr.refr_res[2] = 0.0;
+        cr.refl = refl;
+        cr.transp = transp;
+        cr.R = R;
+        cr.parent = parent;
+        cr.flags = CF_HIT | (slot ? CF_REFRACT_CHILD : 0);
+        A.comb[i] = cr;
+    } else if (valid) {  // finished: color_at = shade_hit with black children, or black on a miss
+        const V3 zero = mk(0.0, 0.0, 0.0);
+        const V3 v = has_hit ? shade_sum(surface, zero, zero, refl, transp, R) : zero;
+        deliver(A.level, i, parent, slot, v, A.out, A.parent_comb, A.level == 0 ? level0_local(A, i) : 0);
+    }
+    flush(cnt, A.counters, W_SHADOW);
 }
 
-// shade_hit's final sum (scene.rs:172-177)
-__device__ __forceinline__ V3 combine3(const CombRec& c) {
-    V3 s = mk(c.surf[0], c.surf[1], c.surf[2]);
-    V3 a = mk(c.refl_res[0], c.refl_res[1], c.refl_res[2]);
-    V3 b = mk(c.refr_res[0], c.refr_res[1], c.refr_res[2]);
-    if (c.refl > 0.0 && c.transp > 0.0) return vadd(vadd(s, vmul(a, c.R)), vmul(b, 1.0 - c.R));
-    return vadd(vadd(s, a), b);
-}
-
-// bottom-up: this level's color_at values -> the parents' reflected/refracted slots, or the canvas
+// bottom-up: the pending events of a level, whose children are all finished, complete their sum
 __global__ void __launch_bounds__(256) combine_kernel(CombArgs C) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= C.n) return;
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= C.n) return;
+    const int64_t i = C.pending[j];
     const CombRec c = C.comb[i];
-    V3 v = (c.flags & CF_HIT) ? combine3(c) : mk(0.0, 0.0, 0.0);
-    if (C.level == 0) {
-        const int64_t ls = C.lrows > 0 ? tile_to_local(C.base + i, C.hs, C.lrows) : C.base + i;
-        double* o = C.out + 3 * ls;
-        o[0] = v.x;
-        o[1] = v.y;
-        o[2] = v.z;
-        return;
-    }
-    CombRec& p = C.parent_comb[c.parent];
-    if (c.flags & CF_REFRACT_CHILD) {  // refracted_color = color_at(...) * transparency
-        double t = p.transp;
-        p.refr_res[0] = v.x * t;
-        p.refr_res[1] = v.y * t;
-        p.refr_res[2] = v.z * t;
-    } else {  // reflected_color = color_at(...) * reflective
-        double t = p.refl;
-        p.refl_res[0] = v.x * t;
-        p.refl_res[1] = v.y * t;
-        p.refl_res[2] = v.z * t;
-    }
+    const V3 v = shade_sum(mk(c.surf[0], c.surf[1], c.surf[2]), mk(c.refl_res[0], c.refl_res[1], c.refl_res[2]),
+                           mk(c.refr_res[0], c.refr_res[1], c.refr_res[2]), c.refl, c.transp, c.R);
+    const int64_t oi = C.level == 0 ? (C.lrows > 0 ? tile_to_local(C.base + i, C.hs, C.lrows) : C.base + i) : 0;
+    deliver(C.level, i, c.parent, (c.flags & CF_REFRACT_CHILD) ? 1 : 0, v, C.out, C.parent_comb, oi);
 }
 
 // canvas.rs:85-96: r = 0.0; r += p (dy outer, dx inner); r /= aa*aa
@@ -536,8 +489,7 @@ struct Span {  // brackets one launch with events when profiling
 }  // namespace
 
 template <bool G, bool LC>
-static void launch_level_t(const DevScene& S, const LevelArgs& A, int64_t n_sr_upper, hipStream_t st,
-                           KernelProf* prof) {
+static void launch_level_t(const DevScene& S, const LevelArgs& A, hipStream_t st, KernelProf* prof) {
     {
         Span s(prof, K_TRACE, st);
         hipLaunchKernelGGL((trace_kernel<G, LC>), dim3(blocks_for(A.n)), dim3(256), cull_lds(S), st, S, A);
@@ -548,31 +500,22 @@ static void launch_level_t(const DevScene& S, const LevelArgs& A, int64_t n_sr_u
     }
     {
         Span s(prof, K_SHADE, st);
-        hipLaunchKernelGGL(shade_kernel, dim3(blocks_for(A.n)), dim3(256), 0, st, S, A);
-    }
-    if (n_sr_upper > 0) {
-        Span s(prof, K_SHADOW, st);
-        hipLaunchKernelGGL((shadow_kernel<G, LC>), dim3(blocks_for(n_sr_upper)), dim3(256), cull_lds(S), st, S, A);
-    }
-    if (S.n_lights > 0) {
-        Span s(prof, K_FINISH, st);
-        hipLaunchKernelGGL(finish_kernel, dim3(blocks_for(A.n)), dim3(256), 0, st, S, A);
+        hipLaunchKernelGGL((shade_kernel<G, LC>), dim3(blocks_for(A.n)), dim3(256), cull_lds(S), st, S, A);
     }
 }
 
-hipError_t launch_level(const DevScene& S, const LevelArgs& A, int64_t n_sr_upper, hipStream_t st,
-                        KernelProf* prof) {
+hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t st, KernelProf* prof) {
     if (A.n <= 0) return hipSuccess;
     if (S.has_groups) {
         if (S.lds_culls)
-            launch_level_t<true, true>(S, A, n_sr_upper, st, prof);
+            launch_level_t<true, true>(S, A, st, prof);
         else
-            launch_level_t<true, false>(S, A, n_sr_upper, st, prof);
+            launch_level_t<true, false>(S, A, st, prof);
     } else {
         if (S.lds_culls)
-            launch_level_t<false, true>(S, A, n_sr_upper, st, prof);
+            launch_level_t<false, true>(S, A, st, prof);
         else
-            launch_level_t<false, false>(S, A, n_sr_upper, st, prof);
+            launch_level_t<false, false>(S, A, st, prof);
     }
     return hipGetLastError();
 }

@@ -1,9 +1,11 @@
 // wavefront.hpp — per-level ray queues of the wavefront render (host + device view).
 //
 // Scene::color_at recursion (scene.rs:128-336) is evaluated level by level: level d holds every
-// pending color_at(ray, max_depth - d).  Each level runs trace -> [n1/n2 walk] -> shade ->
-// shadow -> finish; children (reflected / refracted rays) are appended to level d+1 with a parent
-// link, and a bottom-up combine pass reproduces shade_hit's summation exactly (scene.rs:172-177).
+// pending color_at(ray, max_depth - d).  Each level runs trace -> [n1/n2 walk] -> shade (which
+// includes the shadow walks and the light sum); children (reflected / refracted rays) are appended
+// to level d+1 with a parent link.  Events without children deliver their value at once (canvas or
+// the parent's slot); events with children are listed as pending and a bottom-up combine pass
+// finishes them, reproducing shade_hit's summation exactly (scene.rs:172-177).
 #pragma once
 #include <stdint.h>
 
@@ -25,13 +27,7 @@ struct alignas(16) HitRec {  // closest hit of an event (first t >= 0 of the sor
     int32_t k;     // local entry index (sphere t1 = 0, t2 = 1)
 };
 
-struct alignas(16) ShadeRec {  // Computations subset lighting() needs (computations.rs:13-25)
-    double over[3], eyev[3], normalv[3], pcol[3];
-    int32_t material;
-    int32_t pad;
-};
-
-struct alignas(16) CombRec {  // shade_hit's pending sum
+struct alignas(16) CombRec {  // shade_hit's pending sum (events with children)
     double surf[3];
     double refl_res[3];  // color_at(reflect ray) * reflective, or 0
     double refr_res[3];  // color_at(refract ray) * transparency, or 0
@@ -42,6 +38,6 @@ struct alignas(16) CombRec {  // shade_hit's pending sum
 enum { CF_HIT = 1, CF_REFRACT_CHILD = 2 };
 
 // per-level device counters
-enum { LC_CHILDREN = 0, LC_LIT, LC_N1N2, LC_COUNT };
+enum { LC_CHILDREN = 0, LC_PENDING, LC_N1N2, LC_COUNT };
 
 }  // namespace rr
