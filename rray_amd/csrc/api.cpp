@@ -64,7 +64,7 @@ struct rr_ctx {
     bool has_scene = false;
     rr::HostScene host;
     rr::DevScene S{};
-    DBuf culls, nodes, groups, tris, mats, pats, lights;
+    DBuf culls, chunks, nodes, groups, tris, mats, pats, lights;
     // workspace
     DBuf counters, lcount, hit, n12, n1n2, ev_a, ev_b, canvas, rays0, qout;
     std::vector<DBuf> comb, pend;  // one per level
@@ -147,7 +147,9 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             HIPCHK(c->comb[d].ensure(n * sizeof(rr::CombRec)));
             HIPCHK(c->pend[d].ensure(n * sizeof(int32_t)));
             HIPCHK(c->n1n2.ensure(n * sizeof(int32_t)));
-            const bool children_possible = d < max_depth;
+            // reflected/refracted rays need a reflective or transparent material: without one there is
+            // no level 1, and no host round trip for the child count
+            const bool children_possible = d < max_depth && c->host.has_secondary;
             if (children_possible) HIPCHK(nxt_ev->ensure(2 * n * sizeof(rr::Event)));
             HIPCHK(hipMemsetAsync(c->lcount.p, 0, rr::LC_COUNT * sizeof(unsigned int), st));
             rr::LevelArgs A = base_args;
@@ -315,7 +317,7 @@ void rr_destroy(rr_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (DBuf* b : {&c->culls, &c->nodes, &c->groups, &c->tris, &c->mats, &c->pats, &c->lights, &c->counters,
+    for (DBuf* b : {&c->culls, &c->chunks, &c->nodes, &c->groups, &c->tris, &c->mats, &c->pats, &c->lights, &c->counters,
                     &c->lcount, &c->hit, &c->n12, &c->n1n2, &c->ev_a, &c->ev_b, &c->canvas, &c->rays0, &c->qout})
         b->release();
     for (auto& b : c->comb) b.release();
@@ -338,6 +340,7 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
     HIPCHK(upload(c->culls, hs.culls, st));
+    HIPCHK(upload(c->chunks, hs.chunks, st));
     HIPCHK(upload(c->nodes, hs.nodes, st));
     HIPCHK(upload(c->groups, hs.groups, st));
     HIPCHK(upload(c->tris, hs.tris, st));
@@ -348,6 +351,8 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     c->host = std::move(hs);
     rr::DevScene& S = c->S;
     S.culls = c->culls.as<rr::DevCull>();
+    S.chunks = c->chunks.as<rr::DevChunk>();
+    S.n_chunks = (int32_t)c->host.chunks.size();
     S.nodes = c->nodes.as<rr::DevNode>();
     S.groups = c->groups.as<rr::DevGroup>();
     S.tris = c->tris.as<rr::DevTri>();
@@ -358,7 +363,8 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     S.n_lights = (int32_t)c->host.lights.size();
     S.has_transparent = c->host.has_transparent;
     S.has_groups = c->host.groups.empty() ? 0 : 1;
-    S.lds_culls = (S.n_nodes <= rr::RR_LDS_CULL_CAP && !std::getenv("RRAY_GLOBAL_CULLS")) ? 1 : 0;
+    const size_t lds_bytes = (size_t)S.n_nodes * sizeof(rr::DevCull) + (size_t)S.n_chunks * sizeof(rr::DevChunk);
+    S.lds_culls = (lds_bytes <= (size_t)rr::RR_LDS_CULL_BYTES && !std::getenv("RRAY_GLOBAL_CULLS")) ? 1 : 0;
     c->has_scene = true;
     return RR_OK;
 }

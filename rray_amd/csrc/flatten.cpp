@@ -8,6 +8,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <algorithm>
 #include <functional>
 #include <limits>
 
@@ -106,6 +107,116 @@ DevCull make_cull(const M4& fwd, const double lc[3], double lr) {
     c.c[2] = (float)w.z;
     c.r = (float)r * 1.0001f;
     return c;
+}
+
+uint32_t expand10(uint32_t v) {  // 10 bits -> every third bit
+    v &= 0x3ffu;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+
+// Stores every sibling list in Morton order of its members' cull centres (unbounded members
+// last), keeping each subtree contiguous, and records each node's reference DFS position in
+// `rank`.  The kernels break ties on (t, rank), so results do not depend on the storage order;
+// the spatial order makes runs of consecutive nodes compact, which the chunk culling needs.
+void reorder_spatial(HostScene& hs) {
+    const int N = (int)hs.nodes.size();
+    if (N == 0) return;
+    std::vector<std::vector<int>> kids((size_t)N);
+    std::vector<int> top;
+    for (int i = 0; i < N; ++i) (hs.nodes[i].parent < 0 ? top : kids[hs.nodes[i].parent]).push_back(i);
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    for (const DevCull& c : hs.culls)
+        if (std::isfinite(c.r))
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = std::fmin(lo[k], c.c[k]);
+                hi[k] = std::fmax(hi[k], c.c[k]);
+            }
+    std::vector<uint32_t> key((size_t)N, 0xffffffffu);
+    for (int i = 0; i < N; ++i) {
+        const DevCull& c = hs.culls[i];
+        if (!std::isfinite(c.r)) continue;
+        uint32_t m = 0;
+        for (int k = 0; k < 3; ++k) {
+            double ext = hi[k] - lo[k];
+            double u = ext > 0 ? (c.c[k] - lo[k]) / ext : 0.0;
+            uint32_t q = (uint32_t)std::fmin(1023.0, std::fmax(0.0, std::floor(u * 1024.0)));
+            m |= expand10(q) << k;
+        }
+        key[i] = m;
+    }
+    auto by_key = [&](int a, int b) { return key[a] < key[b]; };
+    std::stable_sort(top.begin(), top.end(), by_key);
+    for (auto& v : kids) std::stable_sort(v.begin(), v.end(), by_key);
+    std::vector<int> perm;
+    perm.reserve((size_t)N);
+    std::function<void(int)> emit = [&](int i) {
+        perm.push_back(i);
+        for (int c : kids[i]) emit(c);
+    };
+    for (int t : top) emit(t);
+    std::vector<int> newidx((size_t)N);
+    for (int k = 0; k < N; ++k) newidx[perm[k]] = k;
+    std::vector<DevNode> nodes((size_t)N);
+    std::vector<DevCull> culls((size_t)N);
+    for (int k = 0; k < N; ++k) {
+        const int o = perm[k];
+        DevNode nd = hs.nodes[o];
+        nd.rank = o;
+        nd.parent = nd.parent >= 0 ? newidx[nd.parent] : -1;
+        nd.skip = k + (hs.nodes[o].skip - o);  // subtree sizes are unchanged
+        nodes[k] = nd;
+        culls[k] = hs.culls[o];
+    }
+    for (DevGroup& g : hs.groups)
+        for (int j = 0; j < RR_MAX_GROUP_DEPTH; ++j)
+            if (g.anc[j] >= 0) g.anc[j] = newidx[g.anc[j]];
+    for (int32_t& v : hs.node_of_object)
+        if (v >= 0) v = newidx[v];
+    hs.nodes.swap(nodes);
+    hs.culls.swap(culls);
+}
+
+// Runs of up to 64 consecutive nodes with a bounding sphere of their culls; unbounded nodes
+// (planes, unbounded groups) get a chunk of their own.
+void build_chunks(HostScene& hs) {
+    hs.chunks.clear();
+    const int N = (int)hs.nodes.size();
+    for (int i = 0; i < N;) {
+        DevChunk ch{};
+        ch.start = i;
+        if (!std::isfinite(hs.culls[i].r)) {
+            ch.count = 1;
+            ch.cull = hs.culls[i];
+            ++i;
+            hs.chunks.push_back(ch);
+            continue;
+        }
+        double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+        int j = i;
+        for (; j < N && j - i < 64 && std::isfinite(hs.culls[j].r); ++j)
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = std::fmin(lo[k], (double)hs.culls[j].c[k] - hs.culls[j].r);
+                hi[k] = std::fmax(hi[k], (double)hs.culls[j].c[k] + hs.culls[j].r);
+            }
+        ch.count = j - i;
+        float cf[3];
+        for (int k = 0; k < 3; ++k) cf[k] = (float)(0.5 * (lo[k] + hi[k]));
+        double r = 0.0;
+        for (int m = i; m < j; ++m) {
+            const DevCull& c = hs.culls[m];
+            double dx = (double)c.c[0] - cf[0], dy = (double)c.c[1] - cf[1], dz = (double)c.c[2] - cf[2];
+            r = std::fmax(r, std::sqrt(dx * dx + dy * dy + dz * dz) + (double)c.r);
+        }
+        for (int k = 0; k < 3; ++k) ch.cull.c[k] = cf[k];
+        ch.cull.r = (float)(r * (1.0 + 1e-6)) * 1.000001f;
+        if (!std::isfinite(ch.cull.r)) ch.cull.r = std::numeric_limits<float>::infinity();
+        hs.chunks.push_back(ch);
+        i = j;
+    }
 }
 
 }  // namespace
@@ -343,8 +454,12 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
         int rc = visit(d.top[i], -1);
         if (rc != RR_OK) return rc;
     }
-    for (const DevNode& nd : out.nodes)
-        if (nd.kind != RR_GROUP && out.mats[nd.material].transparency != 0.0) out.has_transparent = 1;
+    for (const DevNode& nd : out.nodes) {
+        if (nd.kind == RR_GROUP) continue;
+        const DevMaterial& m = out.mats[nd.material];
+        if (m.transparency != 0.0) out.has_transparent = 1;
+        if (m.transparency != 0.0 || m.reflective != 0.0) out.has_secondary = 1;  // scene.rs:281-336
+    }
     // culling bounds (parent space) per node
     std::vector<int> obj_of_node(out.nodes.size(), -1);
     for (int i = 0; i < n; ++i)
@@ -390,6 +505,8 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
         }
         out.culls[ni] = make_cull(world, lc, lr);
     }
+    reorder_spatial(out);
+    build_chunks(out);
     return RR_OK;
 }
 

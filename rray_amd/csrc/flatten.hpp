@@ -11,6 +11,7 @@ namespace rr {
 struct HostScene {
     std::vector<DevNode> nodes;
     std::vector<DevCull> culls;  // one per node
+    std::vector<DevChunk> chunks;
     std::vector<DevGroup> groups;
     std::vector<DevTri> tris;
     std::vector<DevMaterial> mats;
@@ -18,6 +19,7 @@ struct HostScene {
     std::vector<DevLight> lights;
     std::vector<int32_t> node_of_object;  // object id -> node index (-1 if not in the scene tree)
     int32_t has_transparent = 0;
+    int32_t has_secondary = 0;            // some material reflective != 0 or transparency != 0
     int64_t n_top_leaves = 0;             // leaves tested by every ray (reference full scan)
 };
 

@@ -190,6 +190,7 @@ __global__ void __launch_bounds__(256) n1n2_kernel(DevScene S, LevelArgs A) {
     h.t = 0.0;
     h.node = -1;
     h.k = 0;
+    h.rank = 0;
     if (valid) {
         HitRec hr = A.hit[i];
         h.t = hr.t;
@@ -197,6 +198,7 @@ __global__ void __launch_bounds__(256) n1n2_kernel(DevScene S, LevelArgs A) {
         h.v = hr.v;
         h.node = hr.node;
         h.k = hr.k;
+        h.rank = S.nodes[hr.node].rank;
     }
     double n1 = 1.0, n2 = 1.0;
     n1n2_walk<G, LC>(S, r, h, valid, n1, n2, cnt);
@@ -253,6 +255,14 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < A.n;
     Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef RR_STAMPS
+    cnt.st = nullptr;
+    if (A.stamps && A.level == 0) {
+        const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        cnt.st = w < (1 << 16) ? A.stamps + ((int64_t)(1 << 16) + w) * 8 : nullptr;
+    }
+    RR_STAMP(cnt, 0);
+#endif
     HitRec hr;
     hr.node = -1;
     if (valid) hr = A.hit[i];
@@ -312,6 +322,7 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
         R = (m.reflective > 0.0 && m.transparency > 0.0) ? schlick(c) : 0.0;
         event_key(A, i, sample, path);
     }
+    RR_STAMP(cnt, 1);
     // children of this level -> next level queue; parents -> this level's pending list
     const bool pending = do_refl || do_refr;
     {
@@ -350,6 +361,7 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
         }
         if (pending) A.pending[slots[2]] = (int32_t)i;
     }
+    RR_STAMP(cnt, 5);
     // surface = 0 + L0 + L1 + ... (scene.rs:159-166)
     V3 surface = mk(0, 0, 0);
     const DevMaterial m = S.mats[mat];
@@ -380,6 +392,7 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
         }
         if (has_hit) surface = vadd(surface, lighting(m, Lt, pcol, over, eyev, normalv, in_shadow));
     }
+    RR_STAMP(cnt, 6);
     if (pending) {
         CombRec cr;
         cr.surf[0] = surface.x;
@@ -399,6 +412,7 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
         deliver(A.level, i, parent, slot, v, A.out, A.parent_comb, A.level == 0 ? level0_local(A, i) : 0);
     }
     flush(cnt, A.counters, W_SHADOW);
+    RR_STAMP(cnt, 7);
 }
 
 // bottom-up: the pending events of a level, whose children are all finished, complete their sum
@@ -455,7 +469,9 @@ __global__ void __launch_bounds__(256) shadow_query_kernel(DevScene S, const dou
 
 // ------------------------------------------------------------------ host-side launchers
 static inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
-static inline size_t cull_lds(const DevScene& S) { return S.lds_culls ? (size_t)S.n_nodes * sizeof(DevCull) : 0; }
+static inline size_t cull_lds(const DevScene& S) {
+    return S.lds_culls ? (size_t)S.n_nodes * sizeof(DevCull) + (size_t)S.n_chunks * sizeof(DevChunk) : 0;
+}
 
 hipEvent_t KernelProf::get() {
     if (used == pool.size()) {

@@ -26,7 +26,8 @@ struct alignas(16) DevNode {
     int32_t parent;   // parent node index (-1 = scene top level)
     int32_t aux;      // group index (groups) / triangle index (triangles)
     int32_t depth;    // number of group ancestors
-    int32_t pad;
+    int32_t rank;     // position in the reference's DFS order (tie-break key; nodes are stored
+                      // with siblings in spatial order, see flatten.cpp)
 };
 static_assert(sizeof(DevNode) == 128, "DevNode layout");
 
@@ -82,8 +83,16 @@ struct alignas(16) DevCull {
     float r;
 };
 
+// A run of consecutive nodes (<= 64) with the world-space bounding sphere of their culls.
+struct alignas(16) DevChunk {
+    DevCull cull;
+    int32_t start, count;
+    int32_t pad0, pad1;
+};
+
 struct DevScene {
     const DevCull* culls;
+    const DevChunk* chunks;
     const DevNode* nodes;
     const DevGroup* groups;
     const DevTri* tris;
@@ -91,13 +100,16 @@ struct DevScene {
     const DevPattern* pats;
     const DevLight* lights;
     int32_t n_nodes, n_lights;
+    int32_t n_chunks;
+    int32_t pad2;
     int32_t has_transparent;  // any material with transparency != 0 (enables the n1/n2 walk)
     int32_t has_groups;
-    int32_t lds_culls;        // culls staged in LDS per workgroup (n_nodes <= RR_LDS_CULL_CAP)
+    int32_t lds_culls;        // culls + chunks staged in LDS per workgroup (fits in RR_LDS_CULL_BYTES)
     int32_t pad;
 };
-// Up to this many cull records (16 B each) are copied into LDS by every walking workgroup.
-constexpr int RR_LDS_CULL_CAP = 2048;
+// Node culls (16 B each) and chunk records (32 B each) are copied into LDS by every walking
+// workgroup when together they fit in this many bytes.
+constexpr int RR_LDS_CULL_BYTES = 40 * 1024;
 
 // Per-launch counters (u64, zeroed by the host before each launch).
 enum Counter {
