@@ -446,6 +446,7 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     const int64_t rows = part_rows_count(H, o->part, o->nparts, block);
     const int64_t local_rows = rows * o->aa;
     const int64_t total = local_rows * cam->hsize;
+    if (total >= ((int64_t)1 << 31)) return fail(RR_E_LIMIT, "a part must hold fewer than 2^31 samples (use more parts)");
     hipStream_t st = c->stream;
     hipEvent_t ready = nullptr;
     if (hip_stream) {  // order after the caller's stream

@@ -63,6 +63,19 @@ __host__ __device__ inline int64_t tile_to_local(int64_t t, int64_t hs, int64_t 
     const int64_t dy = k / wc;
     return (y0 + dy) * hs + x0 + (k - dy * wc);
 }
+// the same in 32 bits (device: parts hold < 2^31 samples)
+__host__ __device__ inline uint32_t tile_to_local_u32(uint32_t t, uint32_t hs, uint32_t lrows) {
+    const uint32_t band = t / (8u * hs);
+    uint32_t k = t - band * 8u * hs;
+    const uint32_t y0 = band * 8u;
+    const uint32_t hb = lrows - y0 < 8u ? lrows - y0 : 8u;
+    const uint32_t tc = k / (8u * hb);
+    k -= tc * 8u * hb;
+    const uint32_t x0 = tc * 8u;
+    const uint32_t wc = hs - x0 < 8u ? hs - x0 : 8u;
+    const uint32_t dy = k / wc;
+    return (y0 + dy) * hs + x0 + (k - dy * wc);
+}
 
 // Optional per-kernel timing: when `prof` is non-null every launch is bracketed by HIP events on
 // the launch stream and appended to it (resolved on the host after a synchronise).

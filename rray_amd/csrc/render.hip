@@ -16,18 +16,20 @@
 
 namespace rr {
 
-// local sample index of this part -> (px, py) on the supersampled canvas (interleaved row blocks)
-__device__ __forceinline__ void local_to_pixel(const LevelArgs& A, int64_t ls, int64_t& px, int64_t& py) {
-    int64_t lrow = ls / A.hs;
-    px = ls - lrow * A.hs;
-    int64_t k = lrow / A.aa, sub = lrow - k * A.aa;
-    int64_t bi = k / A.block_rows, kb = k - bi * A.block_rows;
-    int64_t y = (bi * A.nparts + A.part) * A.block_rows + kb;
-    py = y * A.aa + sub;
+// local sample index of this part -> (px, py) on the supersampled canvas (interleaved row blocks).
+// 32-bit arithmetic: rr_render_device rejects parts of 2^31 samples or more.
+__device__ __forceinline__ void local_to_pixel(const LevelArgs& A, uint32_t ls, uint32_t& px, uint32_t& py) {
+    const uint32_t hs = (uint32_t)A.hs, aa = (uint32_t)A.aa, br = (uint32_t)A.block_rows;
+    const uint32_t lrow = ls / hs;
+    px = ls - lrow * hs;
+    const uint32_t k = lrow / aa, sub = lrow - k * aa;
+    const uint32_t bi = k / br, kb = k - bi * br;
+    const uint32_t y = (bi * (uint32_t)A.nparts + (uint32_t)A.part) * br + kb;
+    py = y * aa + sub;
 }
 
 // Camera::ray_for_pixel (camera.rs:75-93) with the full 4x4 camera inverse (w included)
-__device__ Ray camera_ray(const DevCamera& C, int64_t px, int64_t py) {
+__device__ Ray camera_ray(const DevCamera& C, uint32_t px, uint32_t py) {
     double xoffset = ((double)px + 0.5) * C.pixel_size;
     double yoffset = ((double)py + 0.5) * C.pixel_size;
     double wx = C.half_width - xoffset;
@@ -44,12 +46,13 @@ __device__ Ray camera_ray(const DevCamera& C, int64_t px, int64_t py) {
 }
 
 // row-major local sample index of level-0 event i (camera events run in tile order)
-__device__ __forceinline__ int64_t level0_local(const LevelArgs& A, int64_t i) {
-    return (A.rays0 || A.lrows <= 0) ? A.base + i : tile_to_local(A.base + i, A.hs, A.lrows);
+__device__ __forceinline__ uint32_t level0_local(const LevelArgs& A, int64_t i) {
+    const uint32_t t = (uint32_t)(A.base + i);
+    return (A.rays0 || A.lrows <= 0) ? t : tile_to_local_u32(t, (uint32_t)A.hs, (uint32_t)A.lrows);
 }
 
-// the ray of event i at this level
-__device__ __forceinline__ Ray event_ray(const LevelArgs& A, int64_t i) {
+// the ray of event i at this level; ls = level0_local(A, i) (used at level 0 only)
+__device__ __forceinline__ Ray event_ray(const LevelArgs& A, int64_t i, uint32_t ls) {
     if (A.level > 0) {
         const Event& e = A.ev[i];
         return {mk(e.o[0], e.o[1], e.o[2]), mk(e.d[0], e.d[1], e.d[2])};
@@ -58,20 +61,24 @@ __device__ __forceinline__ Ray event_ray(const LevelArgs& A, int64_t i) {
         const double* p = A.rays0 + 6 * (A.base + i);
         return {mk(p[0], p[1], p[2]), mk(p[3], p[4], p[5])};
     }
-    int64_t px, py;
-    local_to_pixel(A, level0_local(A, i), px, py);
+    uint32_t px, py;
+    local_to_pixel(A, ls, px, py);
     return camera_ray(A.cam, px, py);
 }
-// jitter identity of event i: (global sample id, recursion path)
-__device__ __forceinline__ void event_key(const LevelArgs& A, int64_t i, uint64_t& sample, uint32_t& path) {
-    int64_t ls = A.level > 0 ? (int64_t)A.ev[i].sample : level0_local(A, i);
+__device__ __forceinline__ Ray event_ray(const LevelArgs& A, int64_t i) {
+    return event_ray(A, i, A.level > 0 ? 0u : level0_local(A, i));
+}
+// jitter identity of event i: (global sample id, recursion path); ls as for event_ray
+__device__ __forceinline__ void event_key(const LevelArgs& A, int64_t i, uint32_t ls0, uint64_t& sample,
+                                          uint32_t& path) {
+    const uint32_t ls = A.level > 0 ? A.ev[i].sample : ls0;
     path = A.level > 0 ? A.ev[i].path : 1u;
     if (A.rays0) {
         sample = (uint64_t)ls;
     } else {
-        int64_t px, py;
+        uint32_t px, py;
         local_to_pixel(A, ls, px, py);
-        sample = (uint64_t)(py * A.hs + px);
+        sample = (uint64_t)py * (uint64_t)A.hs + px;
     }
 }
 
@@ -241,6 +248,66 @@ __device__ __forceinline__ void deliver(int32_t level, int64_t i, int32_t parent
     }
 }
 
+// intensity_at (light.rs:67-96): 1 - in_shadow from is_shadowed toward the light (point) or the
+// fraction of its level^2 jittered cell samples that are shadowed (area, light.rs:47-65)
+template <bool G, bool LC>
+__device__ __forceinline__ double shadow_amount(const DevScene& S, const LevelArgs& A, const DevLight& Lt, int li,
+                                                V3 over, bool active, uint64_t sample, uint32_t path, Counters& cnt) {
+    if (Lt.kind == RR_LIGHT_POINT)
+        return shadowed<G, LC>(S, over, mk(Lt.position[0], Lt.position[1], Lt.position[2]), active, cnt) ? 1.0 : 0.0;
+    const int amount = Lt.level * Lt.level;
+    int total = 0;
+    for (int s = 0; s < amount; ++s) {
+        const int row = s / Lt.level, col = s % Lt.level;
+        double ur = 0.5, vr = 0.5;
+        if (A.jitter_mode == 0) {
+            ur = jitter(A.seed, sample, path, (uint32_t)li, (uint32_t)s, 0);
+            vr = jitter(A.seed, sample, path, (uint32_t)li, (uint32_t)s, 1);
+        }
+        const double uf = ((double)col + ur) / (double)Lt.level;
+        const double vf = ((double)row + vr) / (double)Lt.level;
+        const V3 target = vadd(vadd(mk(Lt.corner[0], Lt.corner[1], Lt.corner[2]), vmul(mk(Lt.u[0], Lt.u[1], Lt.u[2]), uf)),
+                               vmul(mk(Lt.v[0], Lt.v[1], Lt.v[2]), vf));
+        total += shadowed<G, LC>(S, over, target, active, cnt) ? 1 : 0;
+    }
+    return (double)total / (double)amount;
+}
+
+// Per-thread shading state parked in LDS (SoA, 9 doubles x 256 threads = 18 KB) while the shadow
+// walks run, so the walks do not compete with it for VGPRs: eyev, normalv, pattern colour.
+struct ShadeStash {
+    double v[9][256];
+};
+__device__ __forceinline__ void stash_put(ShadeStash& s, V3 eyev, V3 normalv, V3 pcol) {
+    const int t = threadIdx.x;
+    s.v[0][t] = eyev.x;
+    s.v[1][t] = eyev.y;
+    s.v[2][t] = eyev.z;
+    s.v[3][t] = normalv.x;
+    s.v[4][t] = normalv.y;
+    s.v[5][t] = normalv.z;
+    s.v[6][t] = pcol.x;
+    s.v[7][t] = pcol.y;
+    s.v[8][t] = pcol.z;
+}
+
+// one light of shade_hit's sum: surface += lighting(material, light, colour, over, eyev, normalv,
+// intensity_at(light, over)) — the shadow walk first, then the lighting terms from the stash
+template <bool G, bool LC>
+__device__ __forceinline__ void light_step(const DevScene& S, const LevelArgs& A, int li, bool has_hit, int mat,
+                                           V3 over, uint64_t sample, uint32_t path, const ShadeStash& st,
+                                           V3& surface, Counters& cnt) {
+    const DevLight Lt = ldc(S.lights, li);
+    const double in_shadow = shadow_amount<G, LC>(S, A, Lt, li, over, has_hit, sample, path, cnt);
+    if (has_hit) {
+        const int t = threadIdx.x;
+        const V3 eyev = mk(st.v[0][t], st.v[1][t], st.v[2][t]);
+        const V3 normalv = mk(st.v[3][t], st.v[4][t], st.v[5][t]);
+        const V3 pcol = mk(st.v[6][t], st.v[7][t], st.v[8][t]);
+        surface = vadd(surface, lighting(S.mats[mat], Lt, pcol, over, eyev, normalv, in_shadow));
+    }
+}
+
 // Fused shade_hit for every event of the level (scene.rs:159-177):
 //   prepare_computations + pattern (intersection.rs:50-60, material.rs:77-80), the children rays
 //   (reflected_color scene.rs:281-290, refracted_color scene.rs:310-336) appended to level d+1,
@@ -280,8 +347,9 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
     Ray rr = {mk(0, 0, 0), mk(0, 0, 1)}, refr = rr;
     uint64_t sample = 0;
     uint32_t path = 1u;
+    const uint32_t ls0 = A.level > 0 ? 0u : level0_local(A, i);
     if (has_hit) {
-        Ray r = event_ray(A, i);
+        Ray r = event_ray(A, i, ls0);
         Hit h;
         h.found = true;
         h.t = hr.t;
@@ -320,7 +388,7 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
         refl = m.reflective;
         transp = m.transparency;
         R = (m.reflective > 0.0 && m.transparency > 0.0) ? schlick(c) : 0.0;
-        event_key(A, i, sample, path);
+        event_key(A, i, ls0, sample, path);
     }
     RR_STAMP(cnt, 1);
     // children of this level -> next level queue; parents -> this level's pending list
@@ -330,7 +398,7 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
         const bool wq[3] = {do_refl, do_refr, pending};
         int32_t slots[3];
         block_append<3>(ctr, wq, slots);
-        const uint32_t ls = A.level > 0 ? A.ev[valid ? i : 0].sample : (uint32_t)level0_local(A, i);
+        const uint32_t ls = A.level > 0 ? A.ev[valid ? i : 0].sample : ls0;
         if (do_refl) {
             Event e;
             e.o[0] = rr.o.x;
@@ -363,35 +431,11 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
     }
     RR_STAMP(cnt, 5);
     // surface = 0 + L0 + L1 + ... (scene.rs:159-166)
+    __shared__ ShadeStash stash;
+    stash_put(stash, eyev, normalv, pcol);
     V3 surface = mk(0, 0, 0);
-    const DevMaterial m = S.mats[mat];
-    for (int li = 0; li < S.n_lights; ++li) {
-        const DevLight Lt = ldc(S.lights, li);
-        double in_shadow;
-        if (Lt.kind == RR_LIGHT_POINT) {
-            const bool sh = shadowed<G, LC>(S, over, mk(Lt.position[0], Lt.position[1], Lt.position[2]), has_hit, cnt);
-            in_shadow = sh ? 1.0 : 0.0;
-        } else {  // light.rs:47-65: level^2 jittered cell samples
-            const int amount = Lt.level * Lt.level;
-            int total = 0;
-            for (int s = 0; s < amount; ++s) {
-                const int row = s / Lt.level, col = s % Lt.level;
-                double ur = 0.5, vr = 0.5;
-                if (A.jitter_mode == 0) {
-                    ur = jitter(A.seed, sample, path, (uint32_t)li, (uint32_t)s, 0);
-                    vr = jitter(A.seed, sample, path, (uint32_t)li, (uint32_t)s, 1);
-                }
-                const double uf = ((double)col + ur) / (double)Lt.level;
-                const double vf = ((double)row + vr) / (double)Lt.level;
-                const V3 target = vadd(vadd(mk(Lt.corner[0], Lt.corner[1], Lt.corner[2]),
-                                            vmul(mk(Lt.u[0], Lt.u[1], Lt.u[2]), uf)),
-                                       vmul(mk(Lt.v[0], Lt.v[1], Lt.v[2]), vf));
-                total += shadowed<G, LC>(S, over, target, has_hit, cnt) ? 1 : 0;
-            }
-            in_shadow = (double)total / (double)amount;
-        }
-        if (has_hit) surface = vadd(surface, lighting(m, Lt, pcol, over, eyev, normalv, in_shadow));
-    }
+    for (int li = 0; li < S.n_lights; ++li)
+        light_step<G, LC>(S, A, li, has_hit, mat, over, sample, path, stash, surface, cnt);
     RR_STAMP(cnt, 6);
     if (pending) {
         CombRec cr;
@@ -409,7 +453,7 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
     } else if (valid) {  // finished: color_at = shade_hit with black children, or black on a miss
         const V3 zero = mk(0.0, 0.0, 0.0);
         const V3 v = has_hit ? shade_sum(surface, zero, zero, refl, transp, R) : zero;
-        deliver(A.level, i, parent, slot, v, A.out, A.parent_comb, A.level == 0 ? level0_local(A, i) : 0);
+        deliver(A.level, i, parent, slot, v, A.out, A.parent_comb, ls0);
     }
     flush(cnt, A.counters, W_SHADOW);
     RR_STAMP(cnt, 7);
@@ -423,7 +467,8 @@ __global__ void __launch_bounds__(256) combine_kernel(CombArgs C) {
     const CombRec c = C.comb[i];
     const V3 v = shade_sum(mk(c.surf[0], c.surf[1], c.surf[2]), mk(c.refl_res[0], c.refl_res[1], c.refl_res[2]),
                            mk(c.refr_res[0], c.refr_res[1], c.refr_res[2]), c.refl, c.transp, c.R);
-    const int64_t oi = C.level == 0 ? (C.lrows > 0 ? tile_to_local(C.base + i, C.hs, C.lrows) : C.base + i) : 0;
+    const uint32_t t = (uint32_t)(C.base + i);
+    const int64_t oi = C.level == 0 ? (C.lrows > 0 ? tile_to_local_u32(t, (uint32_t)C.hs, (uint32_t)C.lrows) : t) : 0;
     deliver(C.level, i, c.parent, (c.flags & CF_REFRACT_CHILD) ? 1 : 0, v, C.out, C.parent_comb, oi);
 }
 
