@@ -133,10 +133,26 @@ def main():
             traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    # SURVEY §8(d) full-scan model for the same rays: what the reference's algorithm would execute
+    per_ray = (FLOPS["sphere"] * counts["sphere"] + FLOPS["plane"] * counts["plane"] + FLOPS["group"] * counts["group"]
+               + FLOPS["tri"] * counts["tri"])
+    if dom == "trace":
+        ref_flops = stats["rays"] * per_ray
+    elif dom == "n1n2":
+        ref_flops = stats["n1n2_scans"] * per_ray
+    elif dom == "shade":
+        ref_flops = stats["shadow_rays"] * per_ray + stats["shade_events"] * FLOPS["shade"]
+    else:
+        ref_flops = 0
+    ref_tf = ref_flops / (dom_ms / args.steps / 1e3) / 1e12 if dom_ms > 0 else 0.0
     roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": traffic, "kernel": dom,
                 "kernel_ms": round(dom_ms / dom_n, 4), "launches_per_step": launches_per_frame,
                 "flops_per_launch": flops / launches_per_frame,
+                "reference_equivalent": {"tflops": round(ref_tf, 2), "frac": round(ref_tf / FP64_PEAK_TFLOPS, 3),
+                                         "flops_per_step": ref_flops,
+                                         "model": "SURVEY §8(d) full scan (every ray tests every primitive; "
+                                                  "triangles counted as if their group box were hit)"},
                 "note": "achieved = f64 flops the kernel executed: exact leaf tests after culling (SURVEY §8d model: "
                         "sphere 57, plane 13, triangle/group 45) + 250 per shade event for the shade kernel, / kernel "
                         "time; the f32 bundle/line culling that removes the other tests is overhead, not counted. Peak = MI355X FP64 vector = FP64 MFMA "
