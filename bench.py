@@ -3,8 +3,9 @@
 Workload (configs[1]): synthetic 1024-sphere grid + checker plane, point light, 1920x1080, AA=1
 (scenes/c2_s1024.yaml).  One step = one frame rendered to the AA-averaged f64 image in HBM
 (Camera::render + canvas.rs box average, before `as u8`).  With N ranks (torchrun, one process per
-GPU, RCCL) the frame's rows are split in interleaved 8-row blocks and the tiles are gathered to
-rank 0 with one RCCL gather per step ("scaling": "strong": the frame is fixed).
+GPU, RCCL) the frame's rows are split in interleaved 8-row blocks and the tiles (f32) are gathered
+to rank 0 with one RCCL gather per step, double-buffered so the gather of frame k overlaps the
+render of frame k+1 ("scaling": "strong": the frame is fixed).
 
 Also reported: the dominant kernel's roofline (HIP events on the render stream over the timed
 region), and the CPU oracle (test-infrastructure restatement of the reference) timed on a bounded
@@ -48,6 +49,8 @@ def main():
     ap.add_argument("--workload", default="c2_s1024", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-stride", type=int, default=1, help="CPU sample: one 8-row band in every STRIDE bands")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="rehearsal: run the multi-rank path (RCCL process group, pipelined gather) even at 1 rank")
     args = ap.parse_args()
 
     import numpy as np
@@ -58,7 +61,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    if world > 1:
+    multi = world > 1 or args.force_dist
+    if multi:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import rray_amd as R
@@ -72,31 +76,69 @@ def main():
     cam = scene.camera
     block = 8
     rows = R.part_rows(H, rank, world, block)
-    max_rows = max(len(R.part_rows(H, p, world, block)) for p in range(world))
     dev = torch.device("cuda", local)
-    tile = torch.zeros((max_rows, W, 3), dtype=torch.float64, device=dev)
-    frame = torch.empty((H, W, 3), dtype=torch.float64, device=dev) if (world > 1 and rank == 0) else None
     from rray_amd import dist as rdist
-    opts = R._lib.RenderOpts(aa, depth, 0, 0, rank, world, block, R._lib.RR_OUT_AVG)
+    if not multi:
+        # the AA-averaged f64 image (the drop-in's Canvas, before `as u8`)
+        tile = torch.zeros((len(rows), W, 3), dtype=torch.float64, device=dev)
+        opts = R._lib.RenderOpts(aa, depth, 0, 0, rank, world, block, R._lib.RR_OUT_AVG)
 
-    def step():
-        stream = torch.cuda.current_stream(dev).cuda_stream
-        rend.render_device(cam, opts, None, tile.data_ptr(), stream)
-        if world > 1:
-            rdist.gather_frame(tile, H, block, out=frame)
+        side = torch.cuda.Stream(dev) if os.environ.get("RRAY_BENCH_SIDE_STREAM") else None
+
+        def step():
+            stream = (side or torch.cuda.current_stream(dev)).cuda_stream
+            rend.render_device(cam, opts, None, tile.data_ptr(), stream)
+    else:
+        # tiles travel as f32 (the f64 average rounded once; far inside the 1e-5 gate), double-buffered
+        # so that rendering frame k+1 overlaps the RCCL gather of frame k
+        pipe = rdist.FramePipeline(H, W, 3, torch.float32, dev, block=block)
+        opts = R._lib.RenderOpts(aa, depth, 0, 0, rank, world, block, R._lib.RR_OUT_AVG_F32)
+        render_stream = torch.cuda.Stream(dev)
+
+        trace_host = {} if os.environ.get("RRAY_BENCH_TRACE") else None
+
+        def lap(name, t):
+            if trace_host is None:
+                return t
+            now = time.perf_counter()
+            trace_host[name] = trace_host.get(name, 0.0) + now - t
+            return now
+
+        def step():
+            t = time.perf_counter()
+            i, buf, prev = pipe.acquire()
+            with torch.cuda.stream(render_stream):
+                if prev is not None:
+                    prev.wait()  # the gather that last read this buffer
+                t = lap("prev.wait", t)
+                rend.render_device(cam, opts, None, buf.data_ptr(), render_stream.cuda_stream)
+                t = lap("render_device", t)
+            torch.cuda.current_stream(dev).wait_stream(render_stream)
+            t = lap("wait_stream", t)
+            pipe.submit(i)
+            lap("submit", t)
+        tile = None
 
     def sync():
+        if multi:
+            pipe.drain()
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if multi:
             dist.barrier()
 
     for _ in range(args.warmup):
         step()
     sync()
+    if multi and trace_host is not None:
+        trace_host.clear()
     rend.kernel_profile(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    t_enq = time.perf_counter()
+    if world > 1 or args.force_dist:
+        if trace_host is not None:
+            print("host ms/step:", {k: round(v / args.steps * 1e3, 4) for k, v in trace_host.items()}, file=sys.stderr)
     sync()
     t1 = time.perf_counter()
     ktimes = rend.kernel_times()
@@ -177,7 +219,7 @@ def main():
                          f"{args.cpu_stride}), {cpu_samples} samples, {dt:.1f}s"}
         avg = o.aa_average(np.nan_to_num(canvas), aa)
         out_rows = sorted(set(int(y) // aa for y in sel))
-        gpu_img = tile[: len(rows)].cpu().numpy()
+        gpu_img = tile.cpu().numpy() if not multi else pipe.frame.double().cpu().numpy()
         parity = {"rows_checked": len(out_rows),
                   "max_abs_diff": float(np.max(np.abs(gpu_img[out_rows] - avg[out_rows]))),
                   "bit_exact_frac": float(np.mean(gpu_img[out_rows] == avg[out_rows]))}
@@ -189,13 +231,15 @@ def main():
                 "data": "synthetic (scenes/make_scenes.py, seeded)",
                 "config": {"workload": args.workload, "scene": scene_file, "width": W, "height": H, "aa": aa,
                            "max_depth": depth, "samples_per_step": samples_per_frame, "objects": counts["objects"],
-                           "parallelism": f"row-tiles x{world}" + (" + rccl gather" if world > 1 else "")},
+                           "parallelism": f"row-tiles x{world}" + (" + pipelined rccl gather (f32 tiles)"
+                                                                 if world > 1 else "")},
                 "roofline": roofline, "cpu_baseline": cpu, "parity_sample": parity,
                 "kernels_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in ktimes.items() if v[1]},
+                "host_enqueue_ms_per_step": round((t_enq - t0) / args.steps * 1e3, 4),
                 "stats_last_step": {k: stats[k] for k in ("rays", "shadow_rays", "shade_events", "n1n2_scans",
                                                           "prim_tests", "exact_flops", "wave_visits")}}
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if multi:
         dist.barrier()
         dist.destroy_process_group()
     rend.close()

@@ -107,6 +107,8 @@ typedef struct {
 } rr_render_opts;
 #define RR_OUT_CANVAS 1    /* write the supersampled canvas (Canvas.pixels layout) */
 #define RR_OUT_AVG 2       /* write the AA-averaged image (canvas.rs:76-96, before `as u8`) */
+#define RR_OUT_AVG_F32 4   /* rr_render_device only: the AA-averaged image rounded to float (3 floats per
+                              pixel; the average itself is computed in f64) — compact tiles for gathers */
 
 typedef struct {
     uint64_t rays;          /* closest-hit rays (primary + reflected + refracted) */
@@ -145,14 +147,16 @@ int rr_camera_new(int64_t hsize, int64_t vsize, double field_of_view, const doub
 int rr_render(rr_ctx* ctx, const rr_camera* cam, const rr_render_opts* opts, double* out_canvas, double* out_avg,
               rr_stats* stats);
 /* Same, into DEVICE buffers on the context's device, enqueued on `hip_stream` (NULL: ctx stream)
- * and NOT synchronised — for collectives that consume the tile straight from HBM. */
+ * and NOT synchronised — for collectives that consume the tile straight from HBM.  d_avg holds
+ * doubles, or floats with RR_OUT_AVG_F32. */
 int rr_render_device(rr_ctx* ctx, const rr_camera* cam, const rr_render_opts* opts, void* d_canvas, void* d_avg,
                      void* hip_stream);
 /* AA-averaged rows owned by `part` of `nparts` (interleaved blocks of block_rows output rows). */
 int64_t rr_part_rows(int64_t height, int32_t part, int32_t nparts, int32_t block_rows, int64_t* rows_out);
 /* Per-kernel HIP-event timing on the context's stream.  rr_kernel_profile(ctx, 1) resets and enables
  * it; rr_kernel_times fills accumulated milliseconds and launch counts per kernel in the order
- * trace, n1n2, shade, shadow, finish, combine, aa (returns the number of kernels, 7). */
+ * trace, n1n2, shade, shadow, finish, combine, aa (returns the number of kernels, 7; the shadow
+ * walks and the light sum run inside shade, so shadow and finish stay 0). */
 int rr_kernel_profile(rr_ctx* ctx, int enable);
 int rr_kernel_times(rr_ctx* ctx, double* ms, uint64_t* launches, int32_t n);
 /* stats of the last rr_render/rr_render_device on this context (synchronises) */

@@ -14,7 +14,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "rray", "rray.h")
 RR_OK = 0
 ERRORS = {-1: "RR_E_ARG", -2: "RR_E_HIP", -3: "RR_E_SCENE", -4: "RR_E_NONAFFINE", -5: "RR_E_LIMIT", -6: "RR_E_IO",
           -7: "RR_E_NAN"}
-RR_OUT_CANVAS, RR_OUT_AVG = 1, 2
+RR_OUT_CANVAS, RR_OUT_AVG, RR_OUT_AVG_F32 = 1, 2, 4
 SPHERE, PLANE, GROUP, TRIANGLE, SMOOTH_TRIANGLE = range(5)
 PAT = {"test": 0, "solid": 1, "stripe": 2, "gradient": 3, "ring": 4, "checker": 5, "blend": 6}
 LIGHT_POINT, LIGHT_AREA = 0, 1

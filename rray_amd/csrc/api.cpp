@@ -71,6 +71,8 @@ struct rr_ctx {
     unsigned int* h_lcount = nullptr;  // pinned
     unsigned long long* h_counters = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipEvent_t ev_in = nullptr, ev_out = nullptr;
+    hipStream_t last_st = nullptr;  // stream of the last render (the context's workspace is ordered on it)
     rr_stats last{};
     bool stats_pending = false;
     int64_t batch = (int64_t)1 << 23;
@@ -125,10 +127,26 @@ int64_t part_rows_count(int64_t height, int32_t part, int32_t nparts, int32_t bl
 
 // Runs the wavefront levels for `total` level-0 events; level-0 rays come from the camera or from
 // ctx->rays0 (color_at).  Results (color_at values) land in `out` (3 doubles per event).
+// The context's workspace is used on one stream at a time: a call on another stream than the
+// previous one first waits for it (one event, only when the stream changes).
+hipError_t claim_stream(rr_ctx* c, hipStream_t st) {
+    if (c->last_st && c->last_st != st) {
+        hipError_t e = hipEventRecord(c->ev_in, c->last_st);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, c->ev_in, 0);
+        if (e != hipSuccess) return e;
+    }
+    c->last_st = st;
+    return hipSuccess;
+}
+hipError_t sync_ctx(rr_ctx* c) {
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess && c->last_st && c->last_st != c->stream) e = hipStreamSynchronize(c->last_st);
+    return e;
+}
+
 constexpr size_t kCounterBytes = (size_t)rr::RR_CNT_SLOTS * rr::RR_CNT_STRIDE * sizeof(unsigned long long);
 
-int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max_depth, double* out) {
-    hipStream_t st = c->stream;
+int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max_depth, double* out, hipStream_t st) {
     const int64_t B = std::max<int64_t>(1, c->batch);
     for (int64_t base = 0; base < total; base += B) {
         const int64_t nb = std::min(B, total - base);
@@ -262,6 +280,9 @@ int finish_stats(rr_ctx* c) {
     HIPCHK(hipEventSynchronize(c->e1));
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
+    // the counters of the last render stay in HBM until the next one zeroes them: copy on demand
+    // (a per-frame device-to-host copy behind a cross-stream wait blocks the host in HIP)
+    HIPCHK(hipMemcpy(c->h_counters, c->counters.p, kCounterBytes, hipMemcpyDeviceToHost));
     collect_stats(c, &c->last);
     c->last.kernel_ms = ms;
     c->stats_pending = false;
@@ -300,6 +321,8 @@ int rr_create(int device, rr_ctx** out) {
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&c->e0);
     if (e == hipSuccess) e = hipEventCreate(&c->e1);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming);
     if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_lcount, 64 * sizeof(unsigned int), hipHostMallocDefault);
     if (e == hipSuccess)
         e = hipHostMalloc((void**)&c->h_counters, kCounterBytes, hipHostMallocDefault);
@@ -316,7 +339,7 @@ int rr_create(int device, rr_ctx** out) {
 void rr_destroy(rr_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->stream) (void)sync_ctx(c);
     for (DBuf* b : {&c->culls, &c->chunks, &c->nodes, &c->groups, &c->tris, &c->mats, &c->pats, &c->lights, &c->counters,
                     &c->lcount, &c->hit, &c->n12, &c->n1n2, &c->ev_a, &c->ev_b, &c->canvas, &c->rays0, &c->qout})
         b->release();
@@ -327,6 +350,8 @@ void rr_destroy(rr_ctx* c) {
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->e0) (void)hipEventDestroy(c->e0);
     if (c->e1) (void)hipEventDestroy(c->e1);
+    if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+    if (c->ev_out) (void)hipEventDestroy(c->ev_out);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -338,6 +363,7 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     int rc = rr::flatten_scene(*d, hs, err);
     if (rc != RR_OK) return fail(rc, err);
     HIPCHK(hipSetDevice(c->device));
+    HIPCHK(sync_ctx(c));  // renders in flight may still read the previous scene
     hipStream_t st = c->stream;
     HIPCHK(upload(c->culls, hs.culls, st));
     HIPCHK(upload(c->chunks, hs.chunks, st));
@@ -447,13 +473,11 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     const int64_t local_rows = rows * o->aa;
     const int64_t total = local_rows * cam->hsize;
     if (total >= ((int64_t)1 << 31)) return fail(RR_E_LIMIT, "a part must hold fewer than 2^31 samples (use more parts)");
-    hipStream_t st = c->stream;
-    hipEvent_t ready = nullptr;
-    if (hip_stream) {  // order after the caller's stream
-        HIPCHK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-        HIPCHK(hipEventRecord(ready, (hipStream_t)hip_stream));
-        HIPCHK(hipStreamWaitEvent(st, ready, 0));
-    }
+    // Everything is enqueued on the caller's stream (no cross-stream events per call: a HIP event
+    // handoff between streams costs host time every frame).  The context's workspace is reused, so
+    // a render on a different stream than the previous one first waits for that one.
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    HIPCHK(claim_stream(c, st));
     double* canvas = static_cast<double*>(d_canvas);
     if (!canvas) {
         HIPCHK(c->canvas.ensure(std::max<int64_t>(total, 1) * 3 * sizeof(double)));
@@ -472,19 +496,15 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     A.rays0 = nullptr;
     A.seed = o->seed;
     A.jitter_mode = o->jitter_mode;
-    rc = run_levels(c, A, total, o->max_depth, canvas);
+    rc = run_levels(c, A, total, o->max_depth, canvas, st);
     if (rc != RR_OK) return rc;
-    if (d_avg)
+    if (d_avg && (o->flags & RR_OUT_AVG_F32))
+        HIPCHK(rr::launch_aa_f32(canvas, static_cast<float*>(d_avg), W, rows, o->aa, st,
+                                 c->profile ? &c->prof : nullptr));
+    else if (d_avg)
         HIPCHK(rr::launch_aa(canvas, static_cast<double*>(d_avg), W, rows, o->aa, st,
                              c->profile ? &c->prof : nullptr));
     HIPCHK(hipEventRecord(c->e1, st));
-    HIPCHK(hipMemcpyAsync(c->h_counters, c->counters.p, kCounterBytes,
-                          hipMemcpyDeviceToHost, st));
-    if (hip_stream) {  // the caller's stream waits for the tile
-        HIPCHK(hipEventRecord(ready, st));
-        HIPCHK(hipStreamWaitEvent((hipStream_t)hip_stream, ready, 0));
-        HIPCHK(hipEventDestroy(ready));
-    }
     c->stats_pending = true;
     // C_SAMPLES is not incremented by the wavefront kernels; it is the level-0 event count
     c->last.samples = (uint64_t)total;
@@ -493,7 +513,7 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
 
 int rr_kernel_profile(rr_ctx* c, int enable) {
     if (!c) return fail(RR_E_ARG, "null context");
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_ctx(c));
     int rc = resolve_prof(c);
     if (rc != RR_OK) return rc;
     c->profile = enable != 0;
@@ -506,7 +526,7 @@ int rr_kernel_profile(rr_ctx* c, int enable) {
 
 int rr_kernel_times(rr_ctx* c, double* ms, uint64_t* launches, int32_t n) {
     if (!c) return fail(RR_E_ARG, "null context");
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_ctx(c));
     int rc = resolve_prof(c);
     if (rc != RR_OK) return rc;
     for (int k = 0; k < n && k < rr::K_COUNT; ++k) {
@@ -557,6 +577,7 @@ int rr_color_at(rr_ctx* c, int64_t n, const double* origins, const double* direc
     if (n == 0) return RR_OK;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
+    HIPCHK(claim_stream(c, st));
     std::vector<double> rays((size_t)n * 6);
     for (int64_t i = 0; i < n; ++i)
         for (int k = 0; k < 3; ++k) {
@@ -575,7 +596,7 @@ int rr_color_at(rr_ctx* c, int64_t n, const double* origins, const double* direc
     A.rays0 = c->rays0.as<double>();
     A.seed = seed;
     A.jitter_mode = jitter_mode;
-    int rc = run_levels(c, A, n, remaining, c->qout.as<double>());
+    int rc = run_levels(c, A, n, remaining, c->qout.as<double>(), st);
     if (rc != RR_OK) return rc;
     HIPCHK(hipMemcpyAsync(out_rgb, c->qout.p, n * 3 * sizeof(double), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -588,6 +609,7 @@ int rr_is_shadowed(rr_ctx* c, int64_t n, const double* points, const double* lig
     if (n == 0) return RR_OK;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
+    HIPCHK(claim_stream(c, st));
     std::vector<double> buf((size_t)n * 6);
     std::memcpy(buf.data(), points, n * 3 * sizeof(double));
     std::memcpy(buf.data() + 3 * n, light_positions, n * 3 * sizeof(double));

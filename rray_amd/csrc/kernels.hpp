@@ -91,6 +91,8 @@ hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t strea
 hipError_t launch_combine(const CombArgs& C, hipStream_t stream, KernelProf* prof = nullptr);
 hipError_t launch_aa(const double* canvas, double* out, int64_t width, int64_t rows, int32_t aa, hipStream_t stream,
                      KernelProf* prof = nullptr);
+hipError_t launch_aa_f32(const double* canvas, float* out, int64_t width, int64_t rows, int32_t aa, hipStream_t stream,
+                         KernelProf* prof = nullptr);
 hipError_t launch_shadow_query(const DevScene& S, const double* pts, const double* lps, int64_t n, int32_t* out,
                                unsigned long long* counters, hipStream_t stream);
 

@@ -473,7 +473,8 @@ __global__ void __launch_bounds__(256) combine_kernel(CombArgs C) {
 }
 
 // canvas.rs:85-96: r = 0.0; r += p (dy outer, dx inner); r /= aa*aa
-__global__ void __launch_bounds__(256) aa_kernel(const double* __restrict__ canvas, double* __restrict__ out,
+template <class T>
+__global__ void __launch_bounds__(256) aa_kernel(const double* __restrict__ canvas, T* __restrict__ out,
                                                  int64_t width, int64_t rows, int32_t aa) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= width * rows) return;
@@ -488,9 +489,9 @@ __global__ void __launch_bounds__(256) aa_kernel(const double* __restrict__ canv
             g += p[1];
             b += p[2];
         }
-    out[3 * i + 0] = r / total;
-    out[3 * i + 1] = g / total;
-    out[3 * i + 2] = b / total;
+    out[3 * i + 0] = (T)(r / total);
+    out[3 * i + 1] = (T)(g / total);
+    out[3 * i + 2] = (T)(b / total);
 }
 
 // Scene::is_shadowed for caller-given (point, light position) pairs
@@ -588,13 +589,22 @@ hipError_t launch_combine(const CombArgs& C, hipStream_t st, KernelProf* prof) {
     return hipGetLastError();
 }
 
-hipError_t launch_aa(const double* canvas, double* out, int64_t width, int64_t rows, int32_t aa, hipStream_t st,
-                     KernelProf* prof) {
+template <class T>
+static hipError_t launch_aa_t(const double* canvas, T* out, int64_t width, int64_t rows, int32_t aa, hipStream_t st,
+                              KernelProf* prof) {
     int64_t n = width * rows;
     if (n == 0) return hipSuccess;
     Span s(prof, K_AA, st);
-    hipLaunchKernelGGL(aa_kernel, dim3(blocks_for(n)), dim3(256), 0, st, canvas, out, width, rows, aa);
+    hipLaunchKernelGGL((aa_kernel<T>), dim3(blocks_for(n)), dim3(256), 0, st, canvas, out, width, rows, aa);
     return hipGetLastError();
+}
+hipError_t launch_aa(const double* canvas, double* out, int64_t width, int64_t rows, int32_t aa, hipStream_t st,
+                     KernelProf* prof) {
+    return launch_aa_t(canvas, out, width, rows, aa, st, prof);
+}
+hipError_t launch_aa_f32(const double* canvas, float* out, int64_t width, int64_t rows, int32_t aa, hipStream_t st,
+                         KernelProf* prof) {
+    return launch_aa_t(canvas, out, width, rows, aa, st, prof);
 }
 
 template <bool G, bool LC>

@@ -45,6 +45,62 @@ def _worker(rank, world, port, W, H, block, q):
     dist.destroy_process_group()
 
 
+def _pipe_worker(rank, world, port, W, H, block, q):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from oracle.scene_yaml import build_from_yaml
+    from rray_amd import dist as rdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    text = open(os.path.join(ROOT, "scenes", "c3_s1024_reflect.yaml")).read()
+    o, cam = build_from_yaml(text, W, H, 1)
+    canvas, _ = o.render(cam, max_depth=5, threads=2, band=block, band_stride=world, band_phase=rank)
+    rows = rdist.tile_rows(H, rank, world, block)
+    pipe = rdist.FramePipeline(H, W, 3, torch.float32, torch.device("cpu"), block=block)
+    frames = []
+    for k in range(3):  # three frames: both buffers reused once
+        i, tile, prev = pipe.acquire()
+        if prev is not None:
+            prev.wait()
+        tile.zero_()
+        tile[: len(rows)] = torch.from_numpy(canvas[rows] * (k + 1)).float()
+        pipe.submit(i)
+        if rank == 0:
+            frames.append(pipe.frame.clone().numpy())
+    pipe.drain()
+    if rank == 0:
+        q.put(frames)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_pipelined_gather(oracle_mod):
+    from oracle.scene_yaml import build_from_yaml
+
+    import rray_amd  # noqa: F401
+
+    W, H, block, world = 20, 30, 4, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, W, H, block, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frames = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    text = open(os.path.join(ROOT, "scenes", "c3_s1024_reflect.yaml")).read()
+    o, cam = build_from_yaml(text, W, H, 1)
+    full, _ = o.render(cam, max_depth=5, threads=2)
+    for k, fr in enumerate(frames):
+        assert np.array_equal(fr, (full * (k + 1)).astype(np.float32))
+
+
 @pytest.mark.parametrize("world,H", [(2, 36), (2, 33)])
 def test_two_rank_gather_matches_single_render(oracle_mod, world, H):
     from oracle.scene_yaml import build_from_yaml
