@@ -163,6 +163,8 @@ def main():
         flops = stats["exact_flops"][2]
     elif dom == "shade":
         flops = stats["exact_flops"][1] + stats["shade_events"] * FLOPS["shade"]
+    elif dom == "trace_shade":  # fused: closest-hit walk + shading + shadow walks
+        flops = stats["exact_flops"][0] + stats["exact_flops"][1] + stats["shade_events"] * FLOPS["shade"]
     else:
         flops = 0
     launches_per_frame = dom_n / args.steps
@@ -184,6 +186,8 @@ def main():
         ref_flops = stats["n1n2_scans"] * per_ray
     elif dom == "shade":
         ref_flops = stats["shadow_rays"] * per_ray + stats["shade_events"] * FLOPS["shade"]
+    elif dom == "trace_shade":
+        ref_flops = (stats["rays"] + stats["shadow_rays"]) * per_ray + stats["shade_events"] * FLOPS["shade"]
     else:
         ref_flops = 0
     ref_tf = ref_flops / (dom_ms / args.steps / 1e3) / 1e12 if dom_ms > 0 else 0.0

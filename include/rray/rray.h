@@ -155,8 +155,9 @@ int rr_render_device(rr_ctx* ctx, const rr_camera* cam, const rr_render_opts* op
 int64_t rr_part_rows(int64_t height, int32_t part, int32_t nparts, int32_t block_rows, int64_t* rows_out);
 /* Per-kernel HIP-event timing on the context's stream.  rr_kernel_profile(ctx, 1) resets and enables
  * it; rr_kernel_times fills accumulated milliseconds and launch counts per kernel in the order
- * trace, n1n2, shade, shadow, finish, combine, aa (returns the number of kernels, 7; the shadow
- * walks and the light sum run inside shade, so shadow and finish stay 0). */
+ * trace, n1n2, shade, shadow, finish, combine, aa, trace_shade (returns the number of kernels, 8;
+ * the shadow walks and the light sum run inside shade, so shadow and finish stay 0; scenes without
+ * transparent materials run trace and shade as one trace_shade kernel). */
 int rr_kernel_profile(rr_ctx* ctx, int enable);
 int rr_kernel_times(rr_ctx* ctx, double* ms, uint64_t* launches, int32_t n);
 /* stats of the last rr_render/rr_render_device on this context (synchronises) */

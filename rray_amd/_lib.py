@@ -18,7 +18,7 @@ RR_OUT_CANVAS, RR_OUT_AVG, RR_OUT_AVG_F32 = 1, 2, 4
 SPHERE, PLANE, GROUP, TRIANGLE, SMOOTH_TRIANGLE = range(5)
 PAT = {"test": 0, "solid": 1, "stripe": 2, "gradient": 3, "ring": 4, "checker": 5, "blend": 6}
 LIGHT_POINT, LIGHT_AREA = 0, 1
-KERNELS = ["trace", "n1n2", "shade", "shadow", "finish", "combine", "aa"]
+KERNELS = ["trace", "n1n2", "shade", "shadow", "finish", "combine", "aa", "trace_shade"]
 
 _D = C.POINTER(C.c_double)
 _I = C.POINTER(C.c_int32)

@@ -79,7 +79,7 @@ __host__ __device__ inline uint32_t tile_to_local_u32(uint32_t t, uint32_t hs, u
 
 // Optional per-kernel timing: when `prof` is non-null every launch is bracketed by HIP events on
 // the launch stream and appended to it (resolved on the host after a synchronise).
-enum KernelId { K_TRACE = 0, K_N1N2, K_SHADE, K_SHADOW, K_FINISH, K_COMBINE, K_AA, K_COUNT };
+enum KernelId { K_TRACE = 0, K_N1N2, K_SHADE, K_SHADOW, K_FINISH, K_COMBINE, K_AA, K_TRACE_SHADE, K_COUNT };
 struct KernelProf {
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> marks;
     std::vector<hipEvent_t> pool;

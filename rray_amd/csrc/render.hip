@@ -10,6 +10,8 @@
 //   aa_kernel      box average before `as u8`                      canvas.rs:76-96
 // Every kernel is one work-item per queue entry; the node walks inside are wave-uniform (scalar
 // broadcast loads of the flattened scene, culled per wave against the rays' bundle).
+#include <cstdlib>
+
 #include "device_core.inc"
 #include "kernels.hpp"
 #include "wavefront.hpp"
@@ -29,7 +31,7 @@ __device__ __forceinline__ void local_to_pixel(const LevelArgs& A, uint32_t ls, 
 }
 
 // Camera::ray_for_pixel (camera.rs:75-93) with the full 4x4 camera inverse (w included)
-__device__ Ray camera_ray(const DevCamera& C, uint32_t px, uint32_t py) {
+__device__ __forceinline__ Ray camera_ray(const DevCamera& C, uint32_t px, uint32_t py) {
     double xoffset = ((double)px + 0.5) * C.pixel_size;
     double yoffset = ((double)py + 0.5) * C.pixel_size;
     double wx = C.half_width - xoffset;
@@ -273,6 +275,15 @@ __device__ __forceinline__ double shadow_amount(const DevScene& S, const LevelAr
     return (double)total / (double)amount;
 }
 
+// The prelit terms follow the cull records in the walking kernels' dynamic LDS:
+// [light][6 doubles][256 threads] (SoA: lanes of a wave read consecutive doubles).
+constexpr int RR_PRELIT_LIGHTS = 2;
+__device__ __forceinline__ double* prelit_lds(const DevScene& S, bool lc) {
+    char* base = reinterpret_cast<char*>(rr_lds_culls);
+    const size_t off = lc ? (size_t)S.n_nodes * sizeof(DevCull) + (size_t)S.n_chunks * sizeof(DevChunk) : 0;
+    return reinterpret_cast<double*>(base + off);
+}
+
 // Per-thread shading state parked in LDS (SoA, 9 doubles x 256 threads = 18 KB) while the shadow
 // walks run, so the walks do not compete with it for VGPRs: eyev, normalv, pattern colour.
 struct ShadeStash {
@@ -316,12 +327,26 @@ __device__ __forceinline__ void light_step(const DevScene& S, const LevelArgs& A
 // The 64 lanes of a wave walk their shadow rays for the same light sample together, so the walk's
 // ray bundle stays tight.  Events without children are finished here (deliver); events with
 // children store their pending sum and are finished by combine_kernel after their children.
-template <bool G, bool LC>
-__global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
+// FUSED (scenes without transparency, where no n1/n2 walk sits between trace and shade): the
+// kernel first runs the closest-hit walk itself, so the hit and the ray stay in registers.
+// PRE (scenes with <= RR_PRELIT_LIGHTS lights): every light's ambient and diffuse+specular terms
+// (the `pow`-heavy part of lighting) are computed right after prepare_computations and parked in
+// LDS, so the shadow walks run with only the walk state live; otherwise eyev / normalv / colour
+// are parked and lighting runs after each walk.
+// The prelit variant is held to 4 waves/SIMD (<= 128 VGPRs; ~10 VGPRs spill, measured faster than
+// 3 spill-free waves: C2 0.258 vs 0.288 ms/frame).  RR_SHADE_W3 builds the spill-free variant.
+#ifndef RR_SHADE_W3
+#define RR_SHADE_ATTR(PRE) __attribute__((amdgpu_waves_per_eu((PRE) ? 4 : 2)))
+#else
+#define RR_SHADE_ATTR(PRE)
+#endif
+template <bool G, bool LC, bool FUSED, bool PRE>
+__global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE) shade_kernel(DevScene S, LevelArgs A) {
     if (LC) stage_culls(S);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < A.n;
     Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t trace_flops = 0, trace_visits = 0;
 #ifdef RR_STAMPS
     cnt.st = nullptr;
     if (A.stamps && A.level == 0) {
@@ -330,9 +355,26 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
     }
     RR_STAMP(cnt, 0);
 #endif
+    const uint32_t ls0 = A.level > 0 ? 0u : level0_local(A, i);
     HitRec hr;
     hr.node = -1;
-    if (valid) hr = A.hit[i];
+    Ray r0 = {mk(0, 0, 0), mk(0, 0, 1)};  // FUSED: the event's ray, traced here
+    if (FUSED) {
+        if (valid) r0 = event_ray(A, i, ls0);
+        Hit th;
+        trace_closest<G, LC>(S, r0, valid, th, cnt);
+        cnt.rays += popc_ballot(valid);
+        hr.t = th.t;
+        hr.u = th.u;
+        hr.v = th.v;
+        hr.node = th.found ? th.node : -1;
+        hr.k = th.k;
+        trace_flops = cnt.flops;
+        trace_visits = cnt.visits;
+        cnt.flops = cnt.visits = 0;
+    } else if (valid) {
+        hr = A.hit[i];
+    }
     const bool has_hit = valid && hr.node >= 0;
     int32_t parent = -1, slot = 0;
     if (valid && A.level > 0) {
@@ -347,9 +389,8 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
     Ray rr = {mk(0, 0, 0), mk(0, 0, 1)}, refr = rr;
     uint64_t sample = 0;
     uint32_t path = 1u;
-    const uint32_t ls0 = A.level > 0 ? 0u : level0_local(A, i);
     if (has_hit) {
-        Ray r = event_ray(A, i, ls0);
+        const Ray r = FUSED ? r0 : event_ray(A, i, ls0);
         Hit h;
         h.found = true;
         h.t = hr.t;
@@ -366,6 +407,15 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
             c.n2 = A.n12[2 * i + 1];
         }
         pcol = pattern_at(S, m.pattern, world_to_object(S, hr.node, c.over));  // material.rs:77-80
+        if (PRE) {
+            double* pl = prelit_lds(S, LC);
+            for (int li = 0; li < S.n_lights; ++li) {
+                V3 amb, dsp;
+                light_terms(m, ldc(S.lights, li), pcol, c.over, c.eyev, c.normalv, amb, dsp);
+                const double v6[6] = {amb.x, amb.y, amb.z, dsp.x, dsp.y, dsp.z};
+                for (int k = 0; k < 6; ++k) pl[(li * 6 + k) * 256 + threadIdx.x] = v6[k];
+            }
+        }
         over = c.over;
         eyev = c.eyev;
         normalv = c.normalv;
@@ -431,11 +481,25 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
     }
     RR_STAMP(cnt, 5);
     // surface = 0 + L0 + L1 + ... (scene.rs:159-166)
-    __shared__ ShadeStash stash;
-    stash_put(stash, eyev, normalv, pcol);
     V3 surface = mk(0, 0, 0);
-    for (int li = 0; li < S.n_lights; ++li)
-        light_step<G, LC>(S, A, li, has_hit, mat, over, sample, path, stash, surface, cnt);
+    if constexpr (PRE) {
+        const double* pl = prelit_lds(S, LC);
+        for (int li = 0; li < S.n_lights; ++li) {
+            const DevLight Lt = ldc(S.lights, li);
+            const double in_shadow = shadow_amount<G, LC>(S, A, Lt, li, over, has_hit, sample, path, cnt);
+            if (has_hit) {
+                const int t = threadIdx.x;
+                const double* q = pl + li * 6 * 256 + t;
+                const V3 amb = mk(q[0], q[256], q[512]), dsp = mk(q[768], q[1024], q[1280]);
+                surface = vadd(surface, light_final(amb, dsp, in_shadow));
+            }
+        }
+    } else {
+        __shared__ ShadeStash stash;
+        stash_put(stash, eyev, normalv, pcol);
+        for (int li = 0; li < S.n_lights; ++li)
+            light_step<G, LC>(S, A, li, has_hit, mat, over, sample, path, stash, surface, cnt);
+    }
     RR_STAMP(cnt, 6);
     if (pending) {
         CombRec cr;
@@ -456,6 +520,11 @@ __global__ void __launch_bounds__(256) shade_kernel(DevScene S, LevelArgs A) {
         deliver(A.level, i, parent, slot, v, A.out, A.parent_comb, ls0);
     }
     flush(cnt, A.counters, W_SHADOW);
+    if (FUSED && (threadIdx.x & 63) == 0) {
+        unsigned long long* c = A.counters + (blockIdx.x & (RR_CNT_SLOTS - 1)) * RR_CNT_STRIDE;
+        if (trace_flops) atomicAdd(c + C_FLOPS_TRACE, (unsigned long long)trace_flops);
+        if (trace_visits) atomicAdd(c + C_VISITS_TRACE, (unsigned long long)trace_visits);
+    }
     RR_STAMP(cnt, 7);
 }
 
@@ -552,6 +621,16 @@ struct Span {  // brackets one launch with events when profiling
 
 template <bool G, bool LC>
 static void launch_level_t(const DevScene& S, const LevelArgs& A, hipStream_t st, KernelProf* prof) {
+    const bool pre = S.n_lights <= RR_PRELIT_LIGHTS;
+    const size_t shade_lds = cull_lds(S) + (pre ? (size_t)S.n_lights * 6 * 256 * sizeof(double) : 0);
+    if (!S.has_transparent && !std::getenv("RRAY_UNFUSED")) {  // trace + shade in one kernel
+        Span s(prof, K_TRACE_SHADE, st);
+        if (pre)
+            hipLaunchKernelGGL((shade_kernel<G, LC, true, true>), dim3(blocks_for(A.n)), dim3(256), shade_lds, st, S, A);
+        else
+            hipLaunchKernelGGL((shade_kernel<G, LC, true, false>), dim3(blocks_for(A.n)), dim3(256), shade_lds, st, S, A);
+        return;
+    }
     {
         Span s(prof, K_TRACE, st);
         hipLaunchKernelGGL((trace_kernel<G, LC>), dim3(blocks_for(A.n)), dim3(256), cull_lds(S), st, S, A);
@@ -562,7 +641,10 @@ static void launch_level_t(const DevScene& S, const LevelArgs& A, hipStream_t st
     }
     {
         Span s(prof, K_SHADE, st);
-        hipLaunchKernelGGL((shade_kernel<G, LC>), dim3(blocks_for(A.n)), dim3(256), cull_lds(S), st, S, A);
+        if (pre)
+            hipLaunchKernelGGL((shade_kernel<G, LC, false, true>), dim3(blocks_for(A.n)), dim3(256), shade_lds, st, S, A);
+        else
+            hipLaunchKernelGGL((shade_kernel<G, LC, false, false>), dim3(blocks_for(A.n)), dim3(256), shade_lds, st, S, A);
     }
 }
 
