@@ -146,7 +146,8 @@ hipError_t sync_ctx(rr_ctx* c) {
 
 constexpr size_t kCounterBytes = (size_t)rr::RR_CNT_SLOTS * rr::RR_CNT_STRIDE * sizeof(unsigned long long);
 
-int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max_depth, double* out, hipStream_t st) {
+int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max_depth, double* out, hipStream_t st,
+               void* avg = nullptr, int32_t avg_f32 = 0) {
     const int64_t B = std::max<int64_t>(1, c->batch);
     for (int64_t base = 0; base < total; base += B) {
         const int64_t nb = std::min(B, total - base);
@@ -181,6 +182,8 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             A.comb = c->comb[d].as<rr::CombRec>();
             A.parent_comb = d > 0 ? c->comb[d - 1].as<rr::CombRec>() : nullptr;
             A.out = out;
+            A.avg = avg;
+            A.avg_f32 = avg_f32;
             A.next = children_possible ? nxt_ev->as<rr::Event>() : nullptr;
             A.pending = c->pend[d].as<int32_t>();
             A.n1n2_list = c->n1n2.as<int32_t>();
@@ -235,6 +238,8 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             C.comb = c->comb[d].as<rr::CombRec>();
             C.parent_comb = d > 0 ? c->comb[d - 1].as<rr::CombRec>() : nullptr;
             C.out = out;
+            C.avg = avg;
+            C.avg_f32 = avg_f32;
             C.hs = base_args.hs;
             C.lrows = base_args.rays0 ? 0 : base_args.lrows;
             HIPCHK(rr::launch_combine(C, st, c->profile ? &c->prof : nullptr));
@@ -478,8 +483,10 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     // a render on a different stream than the previous one first waits for that one.
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
     HIPCHK(claim_stream(c, st));
+    // aa == 1: the average is written by the kernels directly; the canvas only when asked for
+    const bool direct_avg = o->aa == 1 && d_avg;
     double* canvas = static_cast<double*>(d_canvas);
-    if (!canvas) {
+    if (!canvas && !direct_avg) {
         HIPCHK(c->canvas.ensure(std::max<int64_t>(total, 1) * 3 * sizeof(double)));
         canvas = c->canvas.as<double>();
     }
@@ -496,12 +503,13 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     A.rays0 = nullptr;
     A.seed = o->seed;
     A.jitter_mode = o->jitter_mode;
-    rc = run_levels(c, A, total, o->max_depth, canvas, st);
+    const int32_t f32 = (o->flags & RR_OUT_AVG_F32) ? 1 : 0;
+    rc = run_levels(c, A, total, o->max_depth, canvas, st, direct_avg ? d_avg : nullptr, f32);
     if (rc != RR_OK) return rc;
-    if (d_avg && (o->flags & RR_OUT_AVG_F32))
+    if (d_avg && !direct_avg && f32)
         HIPCHK(rr::launch_aa_f32(canvas, static_cast<float*>(d_avg), W, rows, o->aa, st,
                                  c->profile ? &c->prof : nullptr));
-    else if (d_avg)
+    else if (d_avg && !direct_avg)
         HIPCHK(rr::launch_aa(canvas, static_cast<double*>(d_avg), W, rows, o->aa, st,
                              c->profile ? &c->prof : nullptr));
     HIPCHK(hipEventRecord(c->e1, st));
@@ -558,9 +566,11 @@ int rr_render(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, double* 
     HIPCHK(hipSetDevice(c->device));
     const bool want_avg = (o->flags & RR_OUT_AVG) && out_avg;
     HIPCHK(c->qout.ensure(std::max<int64_t>(W * rows, 1) * 3 * sizeof(double)));
-    rc = rr_render_device(c, cam, o, nullptr, want_avg ? c->qout.p : nullptr, nullptr);
+    const bool want_canvas = (o->flags & RR_OUT_CANVAS) && out_canvas;
+    if (want_canvas) HIPCHK(c->canvas.ensure(std::max<int64_t>(total, 1) * 3 * sizeof(double)));
+    rc = rr_render_device(c, cam, o, want_canvas ? c->canvas.p : nullptr, want_avg ? c->qout.p : nullptr, nullptr);
     if (rc != RR_OK) return rc;
-    if ((o->flags & RR_OUT_CANVAS) && out_canvas)
+    if (want_canvas)
         HIPCHK(hipMemcpyAsync(out_canvas, c->canvas.p, total * 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     if (want_avg)
         HIPCHK(hipMemcpyAsync(out_avg, c->qout.p, W * rows * 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));

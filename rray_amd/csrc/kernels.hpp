@@ -25,7 +25,9 @@ struct LevelArgs {
     double* n12;
     CombRec* comb;           // this level's pending sums (indexed by event)
     CombRec* parent_comb;    // level - 1 (children deliver into their parent's slot)
-    double* out;             // level 0: canvas / color_at results (3 doubles per local sample)
+    double* out;             // level 0: canvas / color_at results (3 doubles per local sample), or null
+    void* avg;               // aa == 1: the averaged image written directly (canvas.rs:85-96 with aa = 1)
+    int32_t avg_f32;         // avg holds floats (RR_OUT_AVG_F32)
     Event* next;
     int32_t* pending;        // this level's events with children
     int32_t* n1n2_list;
@@ -43,7 +45,9 @@ struct CombArgs {
     const int32_t* pending;
     const CombRec* comb;
     CombRec* parent_comb;
-    double* out;  // level 0: canvas (3 doubles per local sample)
+    double* out;  // level 0: canvas (3 doubles per local sample), or null
+    void* avg;    // as LevelArgs
+    int32_t avg_f32;
     int64_t hs, lrows;  // lrows > 0: level-0 events are in tile order (tile_to_local)
 };
 

@@ -227,13 +227,31 @@ __device__ __forceinline__ V3 shade_sum(V3 s, V3 a, V3 b, double refl, double tr
 // A finished color_at value v of event i: level 0 writes the canvas; deeper levels become the
 // parent's reflected_color (v * reflective, scene.rs:281-290) or refracted_color (v * transparency,
 // scene.rs:310-336) slot.  Each slot has exactly one writer.
+// With aa == 1 the box average of canvas.rs:85-96 is r = 0.0; r += p; r /= 1.0, written here
+// directly (same operations) instead of through the canvas and aa_kernel.
 __device__ __forceinline__ void deliver(int32_t level, int64_t i, int32_t parent, int32_t slot, V3 v, double* out,
-                                        CombRec* parent_comb, int64_t out_index) {
+                                        void* avg, int32_t avg_f32, CombRec* parent_comb, int64_t out_index) {
     if (level == 0) {
-        double* o = out + 3 * out_index;
-        o[0] = v.x;
-        o[1] = v.y;
-        o[2] = v.z;
+        if (out) {
+            double* o = out + 3 * out_index;
+            o[0] = v.x;
+            o[1] = v.y;
+            o[2] = v.z;
+        }
+        if (avg) {
+            const double a0 = (0.0 + v.x) / 1.0, a1 = (0.0 + v.y) / 1.0, a2 = (0.0 + v.z) / 1.0;
+            if (avg_f32) {
+                float* o = static_cast<float*>(avg) + 3 * out_index;
+                o[0] = (float)a0;
+                o[1] = (float)a1;
+                o[2] = (float)a2;
+            } else {
+                double* o = static_cast<double*>(avg) + 3 * out_index;
+                o[0] = a0;
+                o[1] = a1;
+                o[2] = a2;
+            }
+        }
         return;
     }
     CombRec& p = parent_comb[parent];
@@ -517,7 +535,7 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE) shade_kernel(DevScene 
     } else if (valid) {  // finished: color_at = shade_hit with black children, or black on a miss
         const V3 zero = mk(0.0, 0.0, 0.0);
         const V3 v = has_hit ? shade_sum(surface, zero, zero, refl, transp, R) : zero;
-        deliver(A.level, i, parent, slot, v, A.out, A.parent_comb, ls0);
+        deliver(A.level, i, parent, slot, v, A.out, A.avg, A.avg_f32, A.parent_comb, ls0);
     }
     flush(cnt, A.counters, W_SHADOW);
     if (FUSED && (threadIdx.x & 63) == 0) {
@@ -538,7 +556,7 @@ __global__ void __launch_bounds__(256) combine_kernel(CombArgs C) {
                            mk(c.refr_res[0], c.refr_res[1], c.refr_res[2]), c.refl, c.transp, c.R);
     const uint32_t t = (uint32_t)(C.base + i);
     const int64_t oi = C.level == 0 ? (C.lrows > 0 ? tile_to_local_u32(t, (uint32_t)C.hs, (uint32_t)C.lrows) : t) : 0;
-    deliver(C.level, i, c.parent, (c.flags & CF_REFRACT_CHILD) ? 1 : 0, v, C.out, C.parent_comb, oi);
+    deliver(C.level, i, c.parent, (c.flags & CF_REFRACT_CHILD) ? 1 : 0, v, C.out, C.avg, C.avg_f32, C.parent_comb, oi);
 }
 
 // canvas.rs:85-96: r = 0.0; r += p (dy outer, dx inner); r /= aa*aa
