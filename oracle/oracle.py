@@ -1,5 +1,6 @@
 """ctypes binding of liboracle (rray_oracle.cpp) — TEST INFRASTRUCTURE ONLY."""
 import ctypes as C
+import math
 import os
 import subprocess
 
@@ -28,7 +29,7 @@ _I = C.POINTER(C.c_int)
 class OrcStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "rays", "shadow_rays", "sphere_tests", "plane_tests", "tri_tests", "group_tests",
-        "group_hits", "shade_events", "nan_sorts")]
+        "group_hits", "cube_tests", "cyl_tests", "cone_tests", "csg_tests", "shade_events", "nan_sorts")]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
@@ -86,6 +87,10 @@ def _load():
         L.orc_jitter.restype = C.c_double
         L.orc_set_context.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_uint64]
         L.orc_get_stats.argtypes = [C.c_void_p, C.POINTER(OrcStats)]
+        L.orc_set_shape_params.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_int]
+        L.orc_set_csg_op.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.orc_csg_allowed.argtypes = [C.c_int] * 4
+        L.orc_csg_filter.argtypes = [C.c_void_p, C.c_int, C.c_int, _D, _I, _I]
         for n in ("orc_mat_identity",):
             getattr(L, n).argtypes = [_D]
         L.orc_mat_translate.argtypes = [C.c_double] * 3 + [_D]
@@ -177,7 +182,9 @@ class Mat:
 DEFAULT_MAT7 = (0.1, 0.9, 0.9, 200.0, 0.0, 0.0, 1.0)  # material.rs:47-58
 
 PAT = {"test": 0, "solid": 1, "stripe": 2, "gradient": 3, "ring": 4, "checker": 5, "blend": 6}
-KIND = {"sphere": 0, "plane": 1, "group": 2, "triangle": 3, "smooth_triangle": 4}
+KIND = {"sphere": 0, "plane": 1, "group": 2, "triangle": 3, "smooth_triangle": 4, "cube": 5, "cylinder": 6,
+        "cone": 7, "csg": 8}
+CSG_OP = {"union": 0, "intersection": 1, "difference": 2}  # csg.rs:13-17
 
 
 class Oracle:
@@ -205,6 +212,27 @@ class Oracle:
         if material is not None or pattern != -1:
             self.set_material(oid, material or DEFAULT_MAT7, pattern)
         return oid
+
+    def set_shape_params(self, oid, minimum=-math.inf, maximum=math.inf, closed=False):
+        """cylinder / cone: minimum, maximum, closed (cylinder.rs:29-37, cone.rs:30-38)"""
+        self.L.orc_set_shape_params(self.w, oid, float(minimum), float(maximum), 1 if closed else 0)
+
+    def add_csg(self, op, parent=-1, transform=None):
+        """CSG; its left and right are the next two objects added with it as parent (csg.rs:51-65)."""
+        oid = self.add("csg", parent, transform)
+        self.L.orc_set_csg_op(self.w, oid, CSG_OP[op] if isinstance(op, str) else op)
+        return oid
+
+    def csg_allowed(self, op, lhit, inl, inr):
+        return bool(self.L.orc_csg_allowed(CSG_OP[op] if isinstance(op, str) else op, int(lhit), int(inl), int(inr)))
+
+    def csg_filter(self, csg, xs):
+        """xs: [(t, obj)] -> indices kept by filter_intersections (csg.rs:82-101)."""
+        n = len(xs)
+        keep = (C.c_int * max(n, 1))()
+        k = self.L.orc_csg_filter(self.w, csg, n, _dv([x[0] for x in xs], max(n, 1)),
+                                  (C.c_int * max(n, 1))(*[x[1] for x in xs]), keep)
+        return [keep[i] for i in range(k)]
 
     def add_triangle(self, p1, p2, p3, parent=-1):
         return self.L.orc_add_triangle(self.w, parent, _dv(p1), _dv(p2), _dv(p3))

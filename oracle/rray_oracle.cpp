@@ -249,6 +249,9 @@ struct Object {
     Material material;
     std::vector<int> children;
     Tuple p1{}, p2{}, p3{}, n1{}, n2{}, n3{}, e1{}, e2{}, normal{};
+    double minimum = -INFINITY, maximum = INFINITY;  // cylinder / cone
+    bool closed = false;
+    int csg_op = 0;  // CSG: children[0] = left, children[1] = right
     bool aabb_valid = false;
     AABB aabb{};
 };
@@ -335,6 +338,26 @@ Tuple local_normal_at(const Object& o, const Tuple& lp, const Intersection& hit)
         case ORC_TRIANGLE: return o.normal;                      // triangle.rs:96-98
         case ORC_SMOOTH_TRIANGLE:                                // smooth_triangle.rs:99-101
             return add(add(mul(o.n2, hit.u), mul(o.n3, hit.v)), mul(o.n1, 1.0 - hit.u - hit.v));
+        case ORC_CUBE: {  // cube.rs:81-90
+            double maxc = std::fmax(std::fmax(std::fabs(lp.x), std::fabs(lp.y)), std::fabs(lp.z));
+            if (maxc == std::fabs(lp.x)) return vector(lp.x, 0.0, 0.0);
+            if (maxc == std::fabs(lp.y)) return vector(0.0, lp.y, 0.0);
+            return vector(0.0, 0.0, lp.z);
+        }
+        case ORC_CYLINDER: {  // cylinder.rs:113-124
+            double dist = lp.x * lp.x + lp.z * lp.z;
+            if (dist < 1.0 && lp.y >= o.maximum - EPSILON) return vector(0.0, 1.0, 0.0);
+            if (dist < 1.0 && lp.y <= o.minimum + EPSILON) return vector(0.0, -1.0, 0.0);
+            return vector(lp.x, 0.0, lp.z);
+        }
+        case ORC_CONE: {  // cone.rs:137-155
+            double dist = lp.x * lp.x + lp.z * lp.z;
+            if (dist < 1.0 && lp.y >= o.maximum - EPSILON) return vector(0.0, 1.0, 0.0);
+            if (dist < 1.0 && lp.y <= o.minimum + EPSILON) return vector(0.0, -1.0, 0.0);
+            double y = std::sqrt(dist);
+            if (lp.y > 0.0) y = -y;
+            return vector(lp.x, y, lp.z);
+        }
         default: return vector(0, 0, 0);  // group.rs: panics ("Groups do not have normals")
     }
 }
@@ -394,6 +417,13 @@ AABB get_aabb(orc_world* w, int id) {
                           std::fmin(o.p1.z, std::fmin(o.p2.z, o.p3.z))),
                     point(std::fmax(o.p1.x, std::fmax(o.p2.x, o.p3.x)), std::fmax(o.p1.y, std::fmax(o.p2.y, o.p3.y)),
                           std::fmax(o.p1.z, std::fmax(o.p2.z, o.p3.z)))};
+        case ORC_CUBE: return {point(-1, -1, -1), point(1, 1, 1)};                   // cube.rs get_aabb
+        case ORC_CYLINDER: return {point(-1, o.minimum, -1), point(1, o.maximum, 1)};  // cylinder.rs get_aabb
+        case ORC_CONE: {                                                          // cone.rs:221-226
+            double limit = std::fmax(std::fabs(o.minimum), std::fabs(o.maximum));
+            return {point(-limit, o.minimum, -limit), point(limit, o.maximum, limit)};
+        }
+        case ORC_CSG:  // csg.rs get_aabb (cached): left then right, transformed
         case ORC_GROUP: {  // group.rs:128-149 (cached)
             if (o.aabb_valid) return o.aabb;
             AABB b{point(INFINITY, INFINITY, INFINITY), point(-INFINITY, -INFINITY, -INFINITY)};
@@ -422,6 +452,41 @@ void sort_xs(std::vector<Intersection>& xs, Ctx& ctx) {
 }
 
 void intersect_obj(const orc_world* w, int id, const Ray& r, std::vector<Intersection>& xs, Ctx& ctx);
+
+// Object::includes: leaves compare ids, groups ask every child (group.rs:151-159), a CSG only
+// compares its two direct children (csg.rs:160-162)
+bool includes(const orc_world* w, int id, int object_id) {
+    const Object& o = w->objects[id];
+    if (o.kind == ORC_GROUP) {
+        for (int c : o.children)
+            if (includes(w, c, object_id)) return true;
+        return false;
+    }
+    if (o.kind == ORC_CSG)
+        return (o.children.size() > 0 && object_id == o.children[0]) ||
+               (o.children.size() > 1 && object_id == o.children[1]);
+    return o.id == object_id;
+}
+bool csg_allowed(int op, bool lhit, bool inl, bool inr) {  // csg.rs:67-80
+    switch (op) {
+        case ORC_CSG_UNION: return (lhit && !inr) || (!lhit && !inl);
+        case ORC_CSG_INTERSECTION: return (lhit && inr) || (!lhit && inl);
+        default: return (lhit && !inr) || (!lhit && inl);  // difference
+    }
+}
+void csg_filter(const orc_world* w, const Object& o, const std::vector<Intersection>& xs,
+                std::vector<Intersection>& out) {  // csg.rs:82-101
+    bool inl = false, inr = false;
+    const int left = o.children.empty() ? -1 : o.children[0];
+    for (const Intersection& i : xs) {
+        bool lhit = left >= 0 && includes(w, left, i.object);
+        if (csg_allowed(o.csg_op, lhit, inl, inr)) out.push_back(i);
+        if (lhit)
+            inl = !inl;
+        else
+            inr = !inr;
+    }
+}
 
 void local_intersect(const orc_world* w, int id, const Ray& ray, std::vector<Intersection>& xs, Ctx& ctx) {
     const Object& o = w->objects[id];
@@ -462,6 +527,94 @@ void local_intersect(const orc_world* w, int id, const Ray& ray, std::vector<Int
             if (v < 0.0 || (u + v) > 1.0) return;
             double t = f * dot(o.e2, oce1);
             xs.push_back({t, o.id, u, v});
+            return;
+        }
+        case ORC_CUBE: {  // cube.rs:64-78
+            ctx.st.cube_tests++;
+            double xtmin, xtmax, ytmin, ytmax, ztmin, ztmax;
+            check_axis(ray.origin.x, ray.direction.x, -1.0, 1.0, xtmin, xtmax);  // cube.rs:49-61
+            check_axis(ray.origin.y, ray.direction.y, -1.0, 1.0, ytmin, ytmax);
+            check_axis(ray.origin.z, ray.direction.z, -1.0, 1.0, ztmin, ztmax);
+            double tmin = std::fmax(std::fmax(xtmin, ytmin), ztmin);
+            double tmax = std::fmin(std::fmin(xtmax, ytmax), ztmax);
+            if (tmin > tmax) return;
+            xs.push_back({tmin, o.id, 0.0, 0.0});
+            xs.push_back({tmax, o.id, 0.0, 0.0});
+            return;
+        }
+        case ORC_CYLINDER: {  // cylinder.rs:85-111
+            ctx.st.cyl_tests++;
+            const Tuple& d = ray.direction;
+            const Tuple& og = ray.origin;
+            double a = d.x * d.x + d.z * d.z;
+            if (std::fabs(a) > EPSILON) {
+                double b = 2.0 * og.x * d.x + 2.0 * og.z * d.z;
+                double c2 = og.x * og.x + og.z * og.z - 1.0;
+                double disc = b * b - 4.0 * a * c2;
+                if (disc < 0.0) return;  // returns vec![] — no caps either
+                double t0 = (-b - std::sqrt(disc)) / (2.0 * a);
+                double t1 = (-b + std::sqrt(disc)) / (2.0 * a);
+                if (t0 > t1) std::swap(t0, t1);
+                double y0 = og.y + t0 * d.y;
+                if (o.minimum < y0 && y0 < o.maximum) xs.push_back({t0, o.id, 0.0, 0.0});
+                double y1 = og.y + t1 * d.y;
+                if (o.minimum < y1 && y1 < o.maximum) xs.push_back({t1, o.id, 0.0, 0.0});
+            }
+            // intersect_caps (cylinder.rs:48-73), check_cap (cylinder.rs:40-46)
+            if (!o.closed || std::fabs(d.y) < EPSILON) return;
+            for (double lim : {o.minimum, o.maximum}) {
+                double t = (lim - og.y) / d.y;
+                double x = og.x + t * d.x, z = og.z + t * d.z;
+                if ((x * x + z * z) <= 1.0) xs.push_back({t, o.id, 0.0, 0.0});
+            }
+            return;
+        }
+        case ORC_CONE: {  // cone.rs:75-135
+            ctx.st.cone_tests++;
+            const Tuple& d = ray.direction;
+            const Tuple& og = ray.origin;
+            auto caps = [&]() {  // cone.rs:46-73, check_cap cone.rs:36-44
+                if (!o.closed || std::fabs(d.y) < EPSILON) return;
+                for (double lim : {o.minimum, o.maximum}) {
+                    double t = (lim - og.y) / d.y;
+                    double x = og.x + t * d.x, y = og.y + t * d.y, z = og.z + t * d.z;
+                    if ((x * x + z * z) <= y * y) xs.push_back({t, o.id, 0.0, 0.0});
+                }
+            };
+            double a = d.x * d.x - d.y * d.y + d.z * d.z;
+            double b = 2.0 * og.x * d.x - 2.0 * og.y * d.y + 2.0 * og.z * d.z;
+            if (std::fabs(a) < EPSILON && std::fabs(b) < EPSILON) {
+                caps();
+                return;
+            }
+            double c2 = og.x * og.x - og.y * og.y + og.z * og.z;
+            if (std::fabs(a) < EPSILON) {
+                double t = -c2 / (2.0 * b);
+                double y = og.y + t * d.y;
+                if (o.minimum < y && y < o.maximum) {
+                    xs.push_back({t, o.id, 0.0, 0.0});
+                    return;  // cone.rs:101-103: returns without the caps
+                }
+            }
+            double disc = b * b - 4.0 * a * c2;
+            if (disc < 0.0) return;
+            double t0 = (-b - std::sqrt(disc)) / (2.0 * a);
+            double t1 = (-b + std::sqrt(disc)) / (2.0 * a);
+            if (t0 > t1) std::swap(t0, t1);
+            double y0 = og.y + t0 * d.y;
+            if (o.minimum < y0 && y0 < o.maximum) xs.push_back({t0, o.id, 0.0, 0.0});
+            double y1 = og.y + t1 * d.y;
+            if (o.minimum < y1 && y1 < o.maximum) xs.push_back({t1, o.id, 0.0, 0.0});
+            caps();
+            return;
+        }
+        case ORC_CSG: {  // csg.rs:105-113: left.intersect ++ right.intersect, sort, filter
+            ctx.st.csg_tests++;
+            std::vector<Intersection> cx;
+            if (o.children.size() >= 1) intersect_obj(w, o.children[0], ray, cx, ctx);
+            if (o.children.size() >= 2) intersect_obj(w, o.children[1], ray, cx, ctx);
+            sort_xs(cx, ctx);
+            csg_filter(w, o, cx, xs);
             return;
         }
         case ORC_GROUP: {  // group.rs:80-91
@@ -744,9 +897,9 @@ void finalize(orc_world* w) {
     if (!w->dirty) return;
     w->dirty = false;
     for (auto& o : w->objects)
-        if (o.kind == ORC_GROUP) o.aabb_valid = false;
+        if (o.kind == ORC_GROUP || o.kind == ORC_CSG) o.aabb_valid = false;
     for (size_t i = 0; i < w->objects.size(); ++i)
-        if (w->objects[i].kind == ORC_GROUP) get_aabb(w, (int)i);
+        if (w->objects[i].kind == ORC_GROUP || w->objects[i].kind == ORC_CSG) get_aabb(w, (int)i);
 }
 
 std::vector<Intersection> xs_from(int n, const double* t, const int* obj, const double* u, const double* v) {
@@ -817,6 +970,25 @@ int orc_add_smooth_triangle(orc_world* w, int parent, const double p1[3], const 
     o.n2 = tp(n2, 0);
     o.n3 = tp(n3, 0);
     return id;
+}
+void orc_set_shape_params(orc_world* w, int id, double minimum, double maximum, int closed) {
+    Object& o = w->objects[id];
+    o.minimum = minimum;
+    o.maximum = maximum;
+    o.closed = closed != 0;
+    w->dirty = true;
+}
+void orc_set_csg_op(orc_world* w, int id, int op) {
+    w->objects[id].csg_op = op;
+    w->dirty = true;
+}
+int orc_csg_allowed(int op, int lhit, int inl, int inr) { return csg_allowed(op, lhit != 0, inl != 0, inr != 0) ? 1 : 0; }
+int orc_csg_filter(orc_world* w, int csg, int n, const double* t, const int* obj, int* keep_index) {
+    std::vector<Intersection> xs, out;
+    for (int i = 0; i < n; ++i) xs.push_back({t[i], obj[i], (double)i, 0.0});  // u carries the index
+    csg_filter(w, w->objects[csg], xs, out);
+    for (size_t k = 0; k < out.size(); ++k) keep_index[k] = (int)out[k].u;
+    return (int)out.size();
 }
 void orc_set_transform(orc_world* w, int id, const double m[16]) {
     Object& o = w->objects[id];
@@ -1077,6 +1249,10 @@ int orc_render(orc_world* w, const orc_camera* c, int max_depth, uint64_t seed, 
             s.tri_tests += x.tri_tests;
             s.group_tests += x.group_tests;
             s.group_hits += x.group_hits;
+            s.cube_tests += x.cube_tests;
+            s.cyl_tests += x.cyl_tests;
+            s.cone_tests += x.cone_tests;
+            s.csg_tests += x.csg_tests;
             s.shade_events += x.shade_events;
             s.nan_sorts += x.nan_sorts;
         }

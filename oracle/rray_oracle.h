@@ -31,12 +31,16 @@ typedef struct orc_world orc_world;
 enum { ORC_PAT_TEST = 0, ORC_PAT_SOLID = 1, ORC_PAT_STRIPE = 2, ORC_PAT_GRADIENT = 3,
        ORC_PAT_RING = 4, ORC_PAT_CHECKER = 5, ORC_PAT_BLEND = 6 };
 /* object kinds */
-enum { ORC_SPHERE = 0, ORC_PLANE = 1, ORC_GROUP = 2, ORC_TRIANGLE = 3, ORC_SMOOTH_TRIANGLE = 4 };
+enum { ORC_SPHERE = 0, ORC_PLANE = 1, ORC_GROUP = 2, ORC_TRIANGLE = 3, ORC_SMOOTH_TRIANGLE = 4,
+       ORC_CUBE = 5, ORC_CYLINDER = 6, ORC_CONE = 7, ORC_CSG = 8 };
+/* CSG operations (csg.rs:13-17) */
+enum { ORC_CSG_UNION = 0, ORC_CSG_INTERSECTION = 1, ORC_CSG_DIFFERENCE = 2 };
 
 typedef struct {
     uint64_t rays;          /* Scene::intersect calls (primary + secondary + shadow) */
     uint64_t shadow_rays;   /* of which from is_shadowed */
     uint64_t sphere_tests, plane_tests, tri_tests, group_tests, group_hits;
+    uint64_t cube_tests, cyl_tests, cone_tests, csg_tests;
     uint64_t shade_events;  /* shade_hit calls */
     uint64_t nan_sorts;     /* sort comparisons that would panic in the reference */
 } orc_stats;
@@ -63,6 +67,13 @@ int  orc_add_smooth_triangle(orc_world* w, int parent, const double p1[3], const
 /* load_obj.rs:124-139 + tobj 4.0.2 semantics; returns the group id or <0 on error */
 int  orc_load_obj(orc_world* w, const char* path, int parent, const double mat7[7], int pattern);
 void orc_set_transform(orc_world* w, int id, const double m[16]);
+/* cylinder / cone: minimum, maximum, closed (cylinder.rs:29-37, cone.rs:30-38) */
+void orc_set_shape_params(orc_world* w, int id, double minimum, double maximum, int closed);
+/* CSG: operation; its left and right are the first and second object added with it as parent */
+void orc_set_csg_op(orc_world* w, int id, int op);
+/* csg.rs:67-80 intersection_allowed; csg.rs:82-101 filter_intersections over (t, obj) */
+int  orc_csg_allowed(int op, int lhit, int inl, int inr);
+int  orc_csg_filter(orc_world* w, int csg, int n, const double* t, const int* obj, int* keep_index);
 /* mat7 = ambient, diffuse, specular, shininess, reflective, transparency, refractive_index */
 void orc_set_material(orc_world* w, int id, const double mat7[7], int pattern /* -1 = default white solid */);
 int  orc_pattern_new(orc_world* w, int kind, const double color[3], int a, int b, double scale, const double m[16]);

@@ -178,13 +178,26 @@ class YamlSceneBuilder:
             for ch in _get(s, "children"):
                 if _get(ch, "hidden") is not True:
                     self.create_shape(ch, oid)
-        elif ty in ("cube", "cylinder", "cone", "torus", "csg"):
-            raise NotImplementedError(f"shape '{ty}' is out of scope (SURVEY.md §2)")
+        elif ty == "cube":
+            oid = o.add("cube", parent)
+        elif ty in ("cylinder", "cone"):  # :332-343
+            oid = o.add(ty, parent)
+            o.set_shape_params(oid, get_f64_default(_get(s, "minimum"), -math.inf),
+                               get_f64_default(_get(s, "maximum"), math.inf), _get(s, "closed") is True)
+        elif ty == "csg":  # :152-162 — left is created (and registered) before right
+            op = _get(s, "operation")
+            if op not in ("union", "intersection", "difference"):
+                raise ValueError(f"Unknown operation: {op}")
+            oid = o.add_csg(op, parent)
+            self.create_shape(_get(s, "left"), oid)
+            self.create_shape(_get(s, "right"), oid)
+        elif ty == "torus":
+            raise NotImplementedError(f"shape '{ty}' is out of scope (SURVEY.md §8 next-4)")
         else:
             raise ValueError(f"Unknown object type: {ty}")
         ts = _get(s, "transforms")
         o.set_transform(oid, create_transforms(ts if isinstance(ts, list) else []))
-        if ty not in ("group", "obj_file"):  # Group::set_material is a no-op (group.rs)
+        if ty not in ("group", "obj_file", "csg"):  # Group/Csg::set_material are no-ops (group.rs, csg.rs)
             # glass_sphere's material (sphere.rs:48-58) is always overwritten by create_material here
             mat7, pat = self.create_material(_get(s, "material"))
             o.set_material(oid, mat7, pat)

@@ -381,3 +381,56 @@ def test_obj_teapot_low(O):  # load_obj.rs:153-158
     w = O()
     g = w.load_obj(os.path.join(here, "golden", "teapot-low.obj"))
     assert w.num_children(g) == 240
+
+
+# ---------------------------------------------------------------- cube.rs / csg.rs unit tests
+def test_ray_intersects_a_cube(oracle_mod):  # cube.rs: ray_intersects_a_cube
+    o = oracle_mod.Oracle()
+    c = o.add("cube")
+    cases = [((5, 0.5, 0), (-1, 0, 0), 4, 6), ((-5, 0.5, 0), (1, 0, 0), 4, 6), ((0.5, 5, 0), (0, -1, 0), 4, 6),
+             ((0.5, -5, 0), (0, 1, 0), 4, 6), ((0.5, 0, 5), (0, 0, -1), 4, 6), ((0.5, 0, -5), (0, 0, 1), 4, 6),
+             ((0, 0.5, 0), (0, 0, 1), -1, 1)]
+    for orig, d, t1, t2 in cases:
+        xs = o.local_intersect(c, orig, d)
+        assert [x[0] for x in xs] == [t1, t2]
+
+
+def test_ray_misses_a_cube(oracle_mod):  # cube.rs: ray_misses_a_cube
+    o = oracle_mod.Oracle()
+    c = o.add("cube")
+    cases = [((-2, 0, 0), (0.2673, 0.5345, 0.8018)), ((0, -2, 0), (0.8018, 0.2673, 0.5345)),
+             ((0, 0, -2), (0.5345, 0.8018, 0.2673)), ((2, 0, 2), (0, 0, -1)), ((0, 2, 2), (0, -1, 0)),
+             ((2, 2, 0), (-1, 0, 0))]
+    for orig, d in cases:
+        assert o.local_intersect(c, orig, d) == []
+
+
+def test_normal_on_the_surface_of_a_cube(oracle_mod):  # cube.rs: normal_on_the_surface_of_a_cube
+    o = oracle_mod.Oracle()
+    c = o.add("cube")
+    cases = [((1, 0.5, -0.8), (1, 0, 0)), ((-1, -0.2, 0.9), (-1, 0, 0)), ((-0.4, 1, -0.1), (0, 1, 0)),
+             ((0.3, -1, -0.7), (0, -1, 0)), ((-0.6, 0.3, 1), (0, 0, 1)), ((0.4, 0.4, -1), (0, 0, -1)),
+             ((1, 1, 1), (1, 0, 0)), ((-1, -1, -1), (-1, 0, 0))]
+    for p, n in cases:
+        assert tuple(o.normal_at(c, p)[:3]) == n  # identity transform: local normal, normalised unit axes
+
+
+def test_evaluating_the_rule_for_a_csg_operation(oracle_mod):  # csg.rs: evaluating_the_rule_...
+    o = oracle_mod.Oracle()
+    table = {"union": [False, True, False, True, False, False, True, True],
+             "intersection": [True, False, True, False, True, True, False, False],
+             "difference": [False, True, False, True, True, True, False, False]}
+    combos = [(True, True, True), (True, True, False), (True, False, True), (True, False, False),
+              (False, True, True), (False, True, False), (False, False, True), (False, False, False)]
+    for op, expect in table.items():
+        assert [o.csg_allowed(op, *c) for c in combos] == expect
+
+
+def test_filtering_a_list_of_intersections(oracle_mod):  # csg.rs: filtering_a_list_of_intersections
+    for op, keep in (("union", [0, 3]), ("intersection", [1, 2]), ("difference", [0, 1])):
+        o = oracle_mod.Oracle()
+        c = o.add_csg(op)
+        s1 = o.add("sphere", c)
+        s2 = o.add("sphere", c)
+        xs = [(1.0, s1), (2.0, s2), (3.0, s1), (4.0, s2)]
+        assert o.csg_filter(c, xs) == keep
