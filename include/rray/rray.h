@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 2
+#define RR_ABI_VERSION 3
 
 /* error codes */
 #define RR_OK 0
@@ -38,8 +38,12 @@ extern "C" {
 #define RR_E_IO (-6)         /* file missing / unreadable / unwritable */
 #define RR_E_NAN (-7)        /* NaN intersection t: reference panics in sort (scene.rs:104) */
 
-/* object kinds — Sphere, Plane, Group, Triangle, SmoothTriangle (src/raytracer/object/) */
-enum { RR_SPHERE = 0, RR_PLANE = 1, RR_GROUP = 2, RR_TRIANGLE = 3, RR_SMOOTH_TRIANGLE = 4 };
+/* object kinds — Sphere, Plane, Group, Triangle, SmoothTriangle, Cube, Cylinder, Cone, Csg
+ * (src/raytracer/object/) */
+enum { RR_SPHERE = 0, RR_PLANE = 1, RR_GROUP = 2, RR_TRIANGLE = 3, RR_SMOOTH_TRIANGLE = 4,
+       RR_CUBE = 5, RR_CYLINDER = 6, RR_CONE = 7, RR_CSG = 8 };
+/* CSG operations — CsgOperation (csg.rs:13-17) */
+enum { RR_CSG_UNION = 0, RR_CSG_INTERSECTION = 1, RR_CSG_DIFFERENCE = 2 };
 /* pattern kinds — PatternType (src/raytracer/material/pattern.rs:10-21), in-scope subset */
 enum { RR_PAT_TEST = 0, RR_PAT_SOLID = 1, RR_PAT_STRIPE = 2, RR_PAT_GRADIENT = 3,
        RR_PAT_RING = 4, RR_PAT_CHECKER = 5, RR_PAT_BLEND = 6 };
@@ -49,6 +53,7 @@ enum { RR_LIGHT_POINT = 0, RR_LIGHT_AREA = 1 };
 #define RR_MAX_DEPTH 8          /* max `remaining` (render uses 5, camera.rs:113) */
 #define RR_MAX_GROUP_DEPTH 6    /* nested group levels */
 #define RR_MAX_PATTERN_DEPTH 8  /* nested pattern levels */
+#define RR_MAX_CSG_ENTRIES 32   /* intersections one CSG subtree can produce for one ray */
 
 /*
  * The scene exactly as the reference's object registry holds it (object/db.rs:11-13 +
@@ -86,6 +91,12 @@ typedef struct {
     const int32_t* light_kind;
     const double* light;         /* n_lights x 15: position, intensity, corner, u, v */
     const int32_t* light_level;  /* area light sample level (light.rs:13) */
+
+    /* ABI 3 */
+    const double* shape;         /* optional n_objects x 3: minimum, maximum, closed (cylinder.rs:29-37,
+                                    cone.rs:30-38); NULL: -inf, +inf, open */
+    const int32_t* csg_op;       /* optional per object: RR_CSG_* (CSG objects; their two children,
+                                    left then right, are the group child lists) */
 } rr_scene_desc;
 
 /* Camera (camera.rs:18-27): hsize/vsize are the SUPERSAMPLED sizes (W*aa, H*aa). */

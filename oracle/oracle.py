@@ -90,6 +90,8 @@ def _load():
         L.orc_set_shape_params.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_int]
         L.orc_set_csg_op.argtypes = [C.c_void_p, C.c_int, C.c_int]
         L.orc_csg_allowed.argtypes = [C.c_int] * 4
+        L.orc_get_shape_params.argtypes = [C.c_void_p, C.c_int, _D]
+        L.orc_get_csg_op.argtypes = [C.c_void_p, C.c_int]
         L.orc_csg_filter.argtypes = [C.c_void_p, C.c_int, C.c_int, _D, _I, _I]
         for n in ("orc_mat_identity",):
             getattr(L, n).argtypes = [_D]
@@ -222,6 +224,14 @@ class Oracle:
         oid = self.add("csg", parent, transform)
         self.L.orc_set_csg_op(self.w, oid, CSG_OP[op] if isinstance(op, str) else op)
         return oid
+
+    def shape_params(self, oid):
+        out = _out(3)
+        self.L.orc_get_shape_params(self.w, oid, out)
+        return list(out)
+
+    def csg_op(self, oid):
+        return self.L.orc_get_csg_op(self.w, oid)
 
     def csg_allowed(self, op, lhit, inl, inr):
         return bool(self.L.orc_csg_allowed(CSG_OP[op] if isinstance(op, str) else op, int(lhit), int(inl), int(inr)))

@@ -982,6 +982,13 @@ void orc_set_csg_op(orc_world* w, int id, int op) {
     w->objects[id].csg_op = op;
     w->dirty = true;
 }
+void orc_get_shape_params(orc_world* w, int id, double out[3]) {
+    const Object& o = w->objects[id];
+    out[0] = o.minimum;
+    out[1] = o.maximum;
+    out[2] = o.closed ? 1.0 : 0.0;
+}
+int orc_get_csg_op(orc_world* w, int id) { return w->objects[id].csg_op; }
 int orc_csg_allowed(int op, int lhit, int inl, int inr) { return csg_allowed(op, lhit != 0, inl != 0, inr != 0) ? 1 : 0; }
 int orc_csg_filter(orc_world* w, int csg, int n, const double* t, const int* obj, int* keep_index) {
     std::vector<Intersection> xs, out;

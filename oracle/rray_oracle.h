@@ -73,6 +73,8 @@ void orc_set_shape_params(orc_world* w, int id, double minimum, double maximum, 
 void orc_set_csg_op(orc_world* w, int id, int op);
 /* csg.rs:67-80 intersection_allowed; csg.rs:82-101 filter_intersections over (t, obj) */
 int  orc_csg_allowed(int op, int lhit, int inl, int inr);
+void orc_get_shape_params(orc_world* w, int id, double out[3]);
+int  orc_get_csg_op(orc_world* w, int id);
 int  orc_csg_filter(orc_world* w, int csg, int n, const double* t, const int* obj, int* keep_index);
 /* mat7 = ambient, diffuse, specular, shininess, reflective, transparency, refractive_index */
 void orc_set_material(orc_world* w, int id, const double mat7[7], int pattern /* -1 = default white solid */);

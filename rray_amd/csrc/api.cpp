@@ -64,7 +64,7 @@ struct rr_ctx {
     bool has_scene = false;
     rr::HostScene host;
     rr::DevScene S{};
-    DBuf culls, chunks, nodes, groups, tris, mats, pats, lights;
+    DBuf culls, chunks, nodes, groups, shapes, tris, mats, pats, lights;
     // workspace
     DBuf counters, lcount, hit, n12, n1n2, ev_a, ev_b, canvas, rays0, qout;
     std::vector<DBuf> comb, pend;  // one per level
@@ -345,7 +345,7 @@ void rr_destroy(rr_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)sync_ctx(c);
-    for (DBuf* b : {&c->culls, &c->chunks, &c->nodes, &c->groups, &c->tris, &c->mats, &c->pats, &c->lights, &c->counters,
+    for (DBuf* b : {&c->culls, &c->chunks, &c->nodes, &c->groups, &c->shapes, &c->tris, &c->mats, &c->pats, &c->lights, &c->counters,
                     &c->lcount, &c->hit, &c->n12, &c->n1n2, &c->ev_a, &c->ev_b, &c->canvas, &c->rays0, &c->qout})
         b->release();
     for (auto& b : c->comb) b.release();
@@ -374,6 +374,7 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     HIPCHK(upload(c->chunks, hs.chunks, st));
     HIPCHK(upload(c->nodes, hs.nodes, st));
     HIPCHK(upload(c->groups, hs.groups, st));
+    HIPCHK(upload(c->shapes, hs.shapes, st));
     HIPCHK(upload(c->tris, hs.tris, st));
     HIPCHK(upload(c->mats, hs.mats, st));
     HIPCHK(upload(c->pats, hs.pats, st));
@@ -386,6 +387,7 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     S.n_chunks = (int32_t)c->host.chunks.size();
     S.nodes = c->nodes.as<rr::DevNode>();
     S.groups = c->groups.as<rr::DevGroup>();
+    S.shapes = c->shapes.as<rr::DevShape>();
     S.tris = c->tris.as<rr::DevTri>();
     S.mats = c->mats.as<rr::DevMaterial>();
     S.pats = c->pats.as<rr::DevPattern>();
@@ -394,6 +396,7 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     S.n_lights = (int32_t)c->host.lights.size();
     S.has_transparent = c->host.has_transparent;
     S.has_groups = c->host.groups.empty() ? 0 : 1;
+    S.general = (c->host.has_csg || c->host.has_quad) ? 1 : 0;
     const size_t lds_bytes = (size_t)S.n_nodes * sizeof(rr::DevCull) + (size_t)S.n_chunks * sizeof(rr::DevChunk);
     S.lds_culls = (lds_bytes <= (size_t)rr::RR_LDS_CULL_BYTES && !std::getenv("RRAY_GLOBAL_CULLS")) ? 1 : 0;
     c->has_scene = true;
@@ -424,7 +427,7 @@ int rr_scene_inspect(const rr_scene_desc* d, double* inverses, double* group_aab
         if (group_aabbs) {
             double* o = group_aabbs + 6 * (size_t)i;
             for (int k = 0; k < 6; ++k) o[k] = 0.0;
-            if (node >= 0 && hs.nodes[node].kind == RR_GROUP)
+            if (node >= 0 && rr::is_container(hs.nodes[node].kind))
                 for (int k = 0; k < 6; ++k) o[k] = hs.groups[hs.nodes[node].aux].aabb[k];
         }
     }

@@ -150,7 +150,19 @@ void reorder_spatial(HostScene& hs) {
     }
     auto by_key = [&](int a, int b) { return key[a] < key[b]; };
     std::stable_sort(top.begin(), top.end(), by_key);
-    for (auto& v : kids) std::stable_sort(v.begin(), v.end(), by_key);
+    // a CSG concatenates left then right and sorts stably (csg.rs:105-113): its subtree keeps the
+    // reference order, so the kernel's in-subtree evaluation order is the reference's
+    std::vector<char> in_csg((size_t)N, 0);
+    for (int i = 0; i < N; ++i)
+        for (int a = hs.nodes[i].parent; a >= 0; a = hs.nodes[a].parent)
+            if (hs.nodes[a].kind == RR_CSG) {
+                in_csg[i] = 1;
+                break;
+            }
+    for (int i = 0; i < N; ++i) {
+        if (in_csg[i]) hs.nodes[i].flags |= NF_IN_CSG;
+        if (hs.nodes[i].kind != RR_CSG && !in_csg[i]) std::stable_sort(kids[i].begin(), kids[i].end(), by_key);
+    }
     std::vector<int> perm;
     perm.reserve((size_t)N);
     std::function<void(int)> emit = [&](int i) {
@@ -327,11 +339,25 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
             return RR_E_NONAFFINE;
         }
         int k = d.kind[i];
-        if (k < RR_SPHERE || k > RR_SMOOTH_TRIANGLE) {
+        if (k < RR_SPHERE || k > RR_CSG) {
             err = "unknown object kind";
             return RR_E_ARG;
         }
-        if (k != RR_GROUP && (d.material[i] < 0 || d.material[i] >= d.n_materials)) {
+        if (k == RR_CSG && (d.child_count ? d.child_count[i] : 0) != 2) {
+            err = "CSG object " + std::to_string(i) + " needs exactly a left and a right child";
+            return RR_E_SCENE;  // csg.rs: get_object(usize::MAX) panics
+        }
+        if (k == RR_CYLINDER || k == RR_CONE) {  // cylinder.rs:29-37, cone.rs:30-38
+            DevShape s{};
+            s.minimum = d.shape ? d.shape[3 * (size_t)i] : -std::numeric_limits<double>::infinity();
+            s.maximum = d.shape ? d.shape[3 * (size_t)i + 1] : std::numeric_limits<double>::infinity();
+            s.closed = d.shape ? (d.shape[3 * (size_t)i + 2] != 0.0) : 0;
+            tri_index[i] = (int)out.shapes.size();
+            out.shapes.push_back(s);
+            out.has_quad = 1;
+        }
+        if (k == RR_CUBE) out.has_quad = 1;  // handled by the general kernel variant
+        if (!is_container(k) && (d.material[i] < 0 || d.material[i] >= d.n_materials)) {
             err = "object " + std::to_string(i) + " has no valid material";
             return RR_E_ARG;
         }
@@ -366,9 +392,15 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
     std::vector<Box> aabb((size_t)n);
     std::function<Box(int, int)> get_aabb = [&](int id, int lvl) -> Box {
         int k = d.kind[id];
-        if (k == RR_SPHERE) return {point(-1, -1, -1), point(1, 1, 1)};            // sphere.rs get_aabb
+        if (k == RR_SPHERE || k == RR_CUBE) return {point(-1, -1, -1), point(1, 1, 1)};  // sphere.rs / cube.rs
         if (k == RR_PLANE) return {point(-inf, 0.0, -inf), point(inf, 0.0, inf)};  // plane.rs get_aabb
-        if (k != RR_GROUP) {                                                       // triangle.rs get_aabb
+        if (k == RR_CYLINDER || k == RR_CONE) {
+            const DevShape& s = out.shapes[tri_index[id]];
+            if (k == RR_CYLINDER) return {point(-1, s.minimum, -1), point(1, s.maximum, 1)};  // cylinder.rs
+            double limit = std::fmax(std::fabs(s.minimum), std::fabs(s.maximum));             // cone.rs:221-226
+            return {point(-limit, s.minimum, -limit), point(limit, s.maximum, limit)};
+        }
+        if (!is_container(k)) {                                                    // triangle.rs get_aabb
             const double* p = d.tri + 18 * (size_t)id;
             return {point(std::fmin(p[0], std::fmin(p[3], p[6])), std::fmin(p[1], std::fmin(p[4], p[7])),
                           std::fmin(p[2], std::fmin(p[5], p[8]))),
@@ -376,7 +408,7 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
                           std::fmax(p[2], std::fmax(p[5], p[8])))};
         }
         if (aabb_state[id] == 2) return aabb[id];
-        Box b{point(inf, inf, inf), point(-inf, -inf, -inf)};  // group.rs:128-149
+        Box b{point(inf, inf, inf), point(-inf, -inf, -inf)};  // group.rs:128-149 (csg.rs: left then right)
         int cs = d.child_start ? d.child_start[id] : 0, cc = d.child_count ? d.child_count[id] : 0;
         for (int j = 0; j < cc && lvl < 64; ++j) {
             int c = d.children[cs + j];
@@ -407,7 +439,7 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
         std::memcpy(nd.inv, &inv12[12 * (size_t)id], sizeof(nd.inv));
         nd.kind = d.kind[id];
         nd.flags = is_identity12(nd.inv) ? NF_IDENT : 0;
-        nd.material = nd.kind == RR_GROUP ? -1 : d.material[id];
+        nd.material = is_container(nd.kind) ? -1 : d.material[id];
         nd.parent = parent_node;
         nd.depth = (int32_t)anc.size();
         nd.aux = tri_index[id];
@@ -416,9 +448,9 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
             return RR_E_ARG;
         }
         out.nodes.push_back(nd);
-        if (nd.kind == RR_GROUP) {
+        if (is_container(nd.kind)) {
             if ((int)anc.size() >= RR_MAX_GROUP_DEPTH) {
-                err = "group nesting exceeds RR_MAX_GROUP_DEPTH";
+                err = "group/CSG nesting exceeds RR_MAX_GROUP_DEPTH";
                 return RR_E_LIMIT;
             }
             anc.push_back(idx);
@@ -432,6 +464,14 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
             g.aabb[5] = b.max.z;
             for (int j = 0; j < RR_MAX_GROUP_DEPTH; ++j) g.anc[j] = j < (int)anc.size() ? anc[j] : -1;
             g.depth = (int32_t)anc.size();
+            g.csg_op = nd.kind == RR_CSG ? (d.csg_op ? d.csg_op[id] : RR_CSG_UNION) : 0;
+            if (nd.kind == RR_CSG) {
+                out.has_csg = 1;
+                if (g.csg_op < RR_CSG_UNION || g.csg_op > RR_CSG_DIFFERENCE) {
+                    err = "unknown CSG operation";
+                    return RR_E_ARG;
+                }
+            }
             out.nodes[idx].aux = (int)out.groups.size();
             out.groups.push_back(g);
             int cs = d.child_start ? d.child_start[id] : 0, cc = d.child_count ? d.child_count[id] : 0;
@@ -455,7 +495,7 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
         if (rc != RR_OK) return rc;
     }
     for (const DevNode& nd : out.nodes) {
-        if (nd.kind == RR_GROUP) continue;
+        if (is_container(nd.kind)) continue;
         const DevMaterial& m = out.mats[nd.material];
         if (m.transparency != 0.0) out.has_transparent = 1;
         if (m.transparency != 0.0 || m.reflective != 0.0) out.has_secondary = 1;  // scene.rs:281-336
@@ -481,8 +521,16 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
                 lr = std::fmax(lr, std::sqrt(dx * dx + dy * dy + dz * dz));
             }
             lr = lr * 1.001 + 1e-9;
-        } else if (nd.kind == RR_GROUP) {
-            const double* b = out.groups[nd.aux].aabb;
+        } else if (nd.kind != RR_PLANE) {  // cube, cylinder, cone: their AABB; group, CSG: the cached AABB
+            double bb[6];
+            if (is_container(nd.kind)) {
+                for (int k = 0; k < 6; ++k) bb[k] = out.groups[nd.aux].aabb[k];
+            } else {
+                Box bx = get_aabb(id, 0);
+                const double v6[6] = {bx.min.x, bx.min.y, bx.min.z, bx.max.x, bx.max.y, bx.max.z};
+                for (int k = 0; k < 6; ++k) bb[k] = v6[k];
+            }
+            const double* b = bb;
             bool finite = true;
             for (int k = 0; k < 6; ++k) finite = finite && std::isfinite(b[k]);
             if (finite && b[0] <= b[3] && b[1] <= b[4] && b[2] <= b[5]) {
@@ -504,6 +552,46 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
             world = multiply(world, inverse(nfull));
         }
         out.culls[ni] = make_cull(world, lc, lr);
+    }
+    // CSG filtering needs left.includes(leaf) for every CSG above a leaf (csg.rs:86-88): leaves compare
+    // ids, groups ask all children (group.rs:151-159), a CSG only its two direct children (csg.rs:160-162)
+    if (out.has_csg) {
+        const int N = (int)out.nodes.size();
+        std::vector<std::vector<int>> kids((size_t)N);
+        for (int i = 0; i < N; ++i)
+            if (out.nodes[i].parent >= 0) kids[out.nodes[i].parent].push_back(i);
+        std::function<bool(int, int)> includes = [&](int c, int leaf) -> bool {
+            const DevNode& cn = out.nodes[c];
+            if (cn.kind == RR_GROUP) {
+                for (int k : kids[c])
+                    if (includes(k, leaf)) return true;
+                return false;
+            }
+            if (cn.kind == RR_CSG) return (kids[c].size() > 0 && kids[c][0] == leaf) || (kids[c].size() > 1 && kids[c][1] == leaf);
+            return c == leaf;
+        };
+        for (int i = 0; i < N; ++i) {
+            DevNode& nd = out.nodes[i];
+            if (is_container(nd.kind) || nd.parent < 0) continue;
+            const DevGroup& g = out.groups[out.nodes[nd.parent].aux];
+            for (int dd = 0; dd < g.depth; ++dd) {
+                const int c = g.anc[dd];
+                if (out.nodes[c].kind == RR_CSG && !kids[c].empty() && includes(kids[c][0], i))
+                    nd.flags |= NF_CSG_LHIT0 << dd;
+            }
+        }
+        for (const DevNode& nd : out.nodes)  // bounded per-ray entry buffer for a CSG subtree
+            if (nd.kind == RR_CSG) {
+                int entries = 0;
+                const int self = (int)(&nd - out.nodes.data());
+                for (int j = self + 1; j < nd.skip; ++j)
+                    if (!is_container(out.nodes[j].kind))
+                        entries += (out.nodes[j].kind == RR_CYLINDER || out.nodes[j].kind == RR_CONE) ? 4 : 2;
+                if (entries > RR_MAX_CSG_ENTRIES) {
+                    err = "a CSG subtree can produce more than RR_MAX_CSG_ENTRIES intersections";
+                    return RR_E_LIMIT;
+                }
+            }
     }
     reorder_spatial(out);
     build_chunks(out);

@@ -14,12 +14,15 @@ struct HostScene {
     std::vector<DevChunk> chunks;
     std::vector<DevGroup> groups;
     std::vector<DevTri> tris;
+    std::vector<DevShape> shapes;
     std::vector<DevMaterial> mats;
     std::vector<DevPattern> pats;
     std::vector<DevLight> lights;
     std::vector<int32_t> node_of_object;  // object id -> node index (-1 if not in the scene tree)
     int32_t has_transparent = 0;
-    int32_t has_secondary = 0;            // some material reflective != 0 or transparency != 0
+    int32_t has_secondary = 0;
+    int32_t has_csg = 0;
+    int32_t has_quad = 0;                 // cubes, cylinders, cones (general kernel variant)            // some material reflective != 0 or transparency != 0
     int64_t n_top_leaves = 0;             // leaves tested by every ray (reference full scan)
 };
 

@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <limits>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -30,6 +31,8 @@ struct rr_scene {
     std::vector<double> pat_color, pat_scale, pat_transform;
     std::vector<int32_t> light_kind, light_level;
     std::vector<double> light;
+    std::vector<double> shape;      // minimum, maximum, closed per object (cylinder / cone)
+    std::vector<int32_t> csg_op;    // per object (CSG)
     rr_scene_desc desc{};
 
     void finalize() {
@@ -68,6 +71,8 @@ struct rr_scene {
         desc.light_kind = light_kind.data();
         desc.light = light.data();
         desc.light_level = light_level.data();
+        desc.shape = shape.data();
+        desc.csg_op = csg_op.data();
     }
 };
 
@@ -203,6 +208,8 @@ struct Builder {
         rr::M4 I = rr::identity();
         S.transform.insert(S.transform.end(), I.m, I.m + 16);
         S.tri.insert(S.tri.end(), 18, 0.0);
+        S.shape.insert(S.shape.end(), {-std::numeric_limits<double>::infinity(), std::numeric_limits<double>::infinity(), 0.0});
+        S.csg_op.push_back(RR_CSG_UNION);
         S.kids.emplace_back();
         if (parent >= 0)
             S.kids[parent].push_back(id);
@@ -239,14 +246,41 @@ struct Builder {
                 const Node& h = ch["hidden"];
                 if (!(h.kind == Node::Bool && h.b)) create_shape(ch, id);
             }
-        } else if (t == "cube" || t == "cylinder" || t == "cone" || t == "torus" || t == "csg") {
-            panic("shape '" + t + "' is outside the GPU path's scope (SURVEY.md §2)", RR_E_LIMIT);
+        } else if (t == "cube") {
+            id = new_object(RR_CUBE, parent);
+        } else if (t == "cylinder" || t == "cone") {  // :332-343
+            const double inf = std::numeric_limits<double>::infinity();
+            const double mn = get_f64_default(s["minimum"], -inf), mx = get_f64_default(s["maximum"], inf);
+            const Node& cl = s["closed"];
+            const bool closed = cl.kind == Node::Bool && cl.b;  // as_bool().unwrap_or(false)
+            id = new_object(t == "cylinder" ? RR_CYLINDER : RR_CONE, parent);
+            S.shape[3 * (size_t)id] = mn;
+            S.shape[3 * (size_t)id + 1] = mx;
+            S.shape[3 * (size_t)id + 2] = closed ? 1.0 : 0.0;
+        } else if (t == "csg") {  // :152-162: operation, then left and right (created in that order)
+            const Node& op = s["operation"];
+            if (op.kind != Node::String) panic("operation not found");
+            int code;
+            if (op.s == "union")
+                code = RR_CSG_UNION;
+            else if (op.s == "intersection")
+                code = RR_CSG_INTERSECTION;
+            else if (op.s == "difference")
+                code = RR_CSG_DIFFERENCE;
+            else
+                panic("Unknown operation: " + op.s);
+            id = new_object(RR_CSG, parent);
+            S.csg_op[id] = code;
+            create_shape(s["left"], id);
+            create_shape(s["right"], id);
+        } else if (t == "torus") {
+            panic("shape 'torus' is outside the GPU path's scope (SURVEY.md §8 next-4)", RR_E_LIMIT);
         } else {
             panic("Unknown object type: " + t);
         }
         set_transform(id, create_transforms(s["transforms"]));
-        int m = create_material(s["material"]);  // Group::set_material is a no-op (group.rs)
-        if (S.kind[id] != RR_GROUP) S.material[id] = m;
+        int m = create_material(s["material"]);  // Group / Csg::set_material are no-ops (group.rs, csg.rs)
+        if (S.kind[id] != RR_GROUP && S.kind[id] != RR_CSG) S.material[id] = m;
         return id;
     }
 };

@@ -134,7 +134,7 @@ __device__ __forceinline__ bool needs_n1n2(const DevMaterial& m, int rem) {
     return m.transparency != 0.0 && (rem > 0 || m.reflective > 0.0);
 }
 
-template <bool G, bool LC>
+template <int G, bool LC>
 __global__ void __launch_bounds__(256) trace_kernel(DevScene S, LevelArgs A) {
     if (LC) stage_culls(S);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(256) trace_kernel(DevScene S, LevelArgs A) {
 #endif
 }
 
-template <bool G, bool LC>
+template <int G, bool LC>
 __global__ void __launch_bounds__(256) n1n2_kernel(DevScene S, LevelArgs A) {
     if (LC) stage_culls(S);
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -270,7 +270,7 @@ __device__ __forceinline__ void deliver(int32_t level, int64_t i, int32_t parent
 
 // intensity_at (light.rs:67-96): 1 - in_shadow from is_shadowed toward the light (point) or the
 // fraction of its level^2 jittered cell samples that are shadowed (area, light.rs:47-65)
-template <bool G, bool LC>
+template <int G, bool LC>
 __device__ __forceinline__ double shadow_amount(const DevScene& S, const LevelArgs& A, const DevLight& Lt, int li,
                                                 V3 over, bool active, uint64_t sample, uint32_t path, Counters& cnt) {
     if (Lt.kind == RR_LIGHT_POINT)
@@ -322,7 +322,7 @@ __device__ __forceinline__ void stash_put(ShadeStash& s, V3 eyev, V3 normalv, V3
 
 // one light of shade_hit's sum: surface += lighting(material, light, colour, over, eyev, normalv,
 // intensity_at(light, over)) — the shadow walk first, then the lighting terms from the stash
-template <bool G, bool LC>
+template <int G, bool LC>
 __device__ __forceinline__ void light_step(const DevScene& S, const LevelArgs& A, int li, bool has_hit, int mat,
                                            V3 over, uint64_t sample, uint32_t path, const ShadeStash& st,
                                            V3& surface, Counters& cnt) {
@@ -358,7 +358,7 @@ __device__ __forceinline__ void light_step(const DevScene& S, const LevelArgs& A
 #else
 #define RR_SHADE_ATTR(PRE)
 #endif
-template <bool G, bool LC, bool FUSED, bool PRE>
+template <int G, bool LC, bool FUSED, bool PRE>
 __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE) shade_kernel(DevScene S, LevelArgs A) {
     if (LC) stage_culls(S);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -582,7 +582,7 @@ __global__ void __launch_bounds__(256) aa_kernel(const double* __restrict__ canv
 }
 
 // Scene::is_shadowed for caller-given (point, light position) pairs
-template <bool G, bool LC>
+template <int G, bool LC>
 __global__ void __launch_bounds__(256) shadow_query_kernel(DevScene S, const double* __restrict__ pts,
                                                            const double* __restrict__ lps, int64_t n,
                                                            int32_t* __restrict__ out, unsigned long long* counters) {
@@ -637,7 +637,7 @@ struct Span {  // brackets one launch with events when profiling
 };
 }  // namespace
 
-template <bool G, bool LC>
+template <int G, bool LC>
 static void launch_level_t(const DevScene& S, const LevelArgs& A, hipStream_t st, KernelProf* prof) {
     const bool pre = S.n_lights <= RR_PRELIT_LIGHTS;
     const size_t shade_lds = cull_lds(S) + (pre ? (size_t)S.n_lights * 6 * 256 * sizeof(double) : 0);
@@ -668,16 +668,22 @@ static void launch_level_t(const DevScene& S, const LevelArgs& A, hipStream_t st
 
 hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t st, KernelProf* prof) {
     if (A.n <= 0) return hipSuccess;
-    if (S.has_groups) {
+    const int g = S.general ? 2 : S.has_groups ? 1 : 0;  // G: flat / groups / general (CSG, 4-entry leaves)
+    if (g == 2) {
         if (S.lds_culls)
-            launch_level_t<true, true>(S, A, st, prof);
+            launch_level_t<2, true>(S, A, st, prof);
         else
-            launch_level_t<true, false>(S, A, st, prof);
+            launch_level_t<2, false>(S, A, st, prof);
+    } else if (g == 1) {
+        if (S.lds_culls)
+            launch_level_t<1, true>(S, A, st, prof);
+        else
+            launch_level_t<1, false>(S, A, st, prof);
     } else {
         if (S.lds_culls)
-            launch_level_t<false, true>(S, A, st, prof);
+            launch_level_t<0, true>(S, A, st, prof);
         else
-            launch_level_t<false, false>(S, A, st, prof);
+            launch_level_t<0, false>(S, A, st, prof);
     }
     return hipGetLastError();
 }
@@ -707,7 +713,7 @@ hipError_t launch_aa_f32(const double* canvas, float* out, int64_t width, int64_
     return launch_aa_t(canvas, out, width, rows, aa, st, prof);
 }
 
-template <bool G, bool LC>
+template <int G, bool LC>
 static void launch_shadow_query_t(const DevScene& S, const double* pts, const double* lps, int64_t n, int32_t* out,
                                   unsigned long long* counters, hipStream_t st) {
     hipLaunchKernelGGL((shadow_query_kernel<G, LC>), dim3(blocks_for(n)), dim3(256), cull_lds(S), st, S, pts, lps, n, out,
@@ -717,16 +723,22 @@ static void launch_shadow_query_t(const DevScene& S, const double* pts, const do
 hipError_t launch_shadow_query(const DevScene& S, const double* pts, const double* lps, int64_t n, int32_t* out,
                                unsigned long long* counters, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    if (S.has_groups) {
+    const int g = S.general ? 2 : S.has_groups ? 1 : 0;
+    if (g == 2) {
         if (S.lds_culls)
-            launch_shadow_query_t<true, true>(S, pts, lps, n, out, counters, st);
+            launch_shadow_query_t<2, true>(S, pts, lps, n, out, counters, st);
         else
-            launch_shadow_query_t<true, false>(S, pts, lps, n, out, counters, st);
+            launch_shadow_query_t<2, false>(S, pts, lps, n, out, counters, st);
+    } else if (g == 1) {
+        if (S.lds_culls)
+            launch_shadow_query_t<1, true>(S, pts, lps, n, out, counters, st);
+        else
+            launch_shadow_query_t<1, false>(S, pts, lps, n, out, counters, st);
     } else {
         if (S.lds_culls)
-            launch_shadow_query_t<false, true>(S, pts, lps, n, out, counters, st);
+            launch_shadow_query_t<0, true>(S, pts, lps, n, out, counters, st);
         else
-            launch_shadow_query_t<false, false>(S, pts, lps, n, out, counters, st);
+            launch_shadow_query_t<0, false>(S, pts, lps, n, out, counters, st);
     }
     return hipGetLastError();
 }

@@ -13,8 +13,12 @@
 namespace rr {
 
 enum NodeFlags : int32_t {
-    NF_IDENT = 1,  // inverse transform is exactly the identity (skip the ray transform)
+    NF_IDENT = 1,       // inverse transform is exactly the identity (skip the ray transform)
+    NF_IN_CSG = 2,      // inside a CSG subtree: intersected only through the CSG's evaluation
+    NF_CSG_LHIT0 = 256, // bit (8 + d): for the CSG at position d of this leaf's ancestor chain,
+                        // left.includes(this leaf) (csg.rs:86-88 with Object::includes semantics)
 };
+__host__ __device__ inline bool is_container(int kind) { return kind == RR_GROUP || kind == RR_CSG; }
 
 // One flattened object.  128 B, 16-B aligned.
 struct alignas(16) DevNode {
@@ -31,11 +35,19 @@ struct alignas(16) DevNode {
 };
 static_assert(sizeof(DevNode) == 128, "DevNode layout");
 
-// Per group: bounding box in the group's own space (group.rs:128-149) and its ancestor chain.
+// Per group / CSG: bounding box in its own space (group.rs:128-149, csg.rs get_aabb) and its
+// ancestor chain (groups and CSGs).
 struct alignas(16) DevGroup {
     double aabb[6];                      // min xyz, max xyz
-    int32_t anc[RR_MAX_GROUP_DEPTH];     // node indices root-first; anc[depth-1] == this group
-    int32_t depth;                       // number of groups from the root down to and incl. this one
+    int32_t anc[RR_MAX_GROUP_DEPTH];     // node indices root-first; anc[depth-1] == this node
+    int32_t depth;                       // number of containers from the root down to and incl. this one
+    int32_t csg_op;                      // RR_CSG_* (CSG nodes)
+};
+
+// Cylinder / cone parameters (cylinder.rs:29-37, cone.rs:30-38).
+struct alignas(16) DevShape {
+    double minimum, maximum;
+    int32_t closed;
     int32_t pad;
 };
 
@@ -99,13 +111,14 @@ struct DevScene {
     const DevMaterial* mats;
     const DevPattern* pats;
     const DevLight* lights;
+    const DevShape* shapes;
     int32_t n_nodes, n_lights;
     int32_t n_chunks;
     int32_t pad2;
     int32_t has_transparent;  // any material with transparency != 0 (enables the n1/n2 walk)
     int32_t has_groups;
+    int32_t general;          // CSGs or cylinders / cones present: the kernels' G = 2 variant
     int32_t lds_culls;        // culls + chunks staged in LDS per workgroup (fits in RR_LDS_CULL_BYTES)
-    int32_t pad;
 };
 // Node culls (16 B each) and chunk records (32 B each) are copied into LDS by every walking
 // workgroup when together they fit in this many bytes.

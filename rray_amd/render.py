@@ -8,6 +8,7 @@ Reference names kept where they exist:
 Every call goes to librray_amd.so's HIP kernels; there is no CPU path.
 """
 import ctypes as C
+import math
 
 import numpy as np
 
@@ -34,6 +35,7 @@ class SceneBuilder:
         self.mats, self.mat_pattern = [], []
         self.pat_kind, self.pat_a, self.pat_b, self.pat_color, self.pat_scale, self.pat_transform = [], [], [], [], [], []
         self.light_kind, self.light, self.light_level = [], [], []
+        self.shape, self.csg_op = [], []
         self._keep = None
 
     # --- materials / patterns (material.rs, pattern.rs)
@@ -56,7 +58,7 @@ class SceneBuilder:
         oid = len(self.kind)
         self.kind.append(kind)
         self.parent.append(parent)
-        if kind == _lib.GROUP:
+        if kind in (_lib.GROUP, _lib.CSG):
             self.material.append(-1)
         else:
             self.material.append(material if isinstance(material, int) else self.new_material(
@@ -64,6 +66,8 @@ class SceneBuilder:
         self.transform.extend(float(x) for x in (transform or IDENTITY))
         self.tri.extend([float(x) for x in tri] if tri is not None else [0.0] * 18)
         self.kids.append([])
+        self.shape.extend([-math.inf, math.inf, 0.0])
+        self.csg_op.append(0)
         (self.kids[parent] if parent >= 0 else self.top).append(oid)
         return oid
 
@@ -75,6 +79,25 @@ class SceneBuilder:
 
     def group(self, transform=None, parent=-1):
         return self._obj(_lib.GROUP, parent, transform, None, -1)
+
+    def cube(self, transform=None, material=None, pattern=-1, parent=-1):
+        return self._obj(_lib.CUBE, parent, transform, material, pattern)
+
+    def cylinder(self, minimum=-math.inf, maximum=math.inf, closed=False, transform=None, material=None, pattern=-1,
+                 parent=-1, cone=False):
+        oid = self._obj(_lib.CONE if cone else _lib.CYLINDER, parent, transform, material, pattern)
+        self.shape[3 * oid:3 * oid + 3] = [float(minimum), float(maximum), 1.0 if closed else 0.0]
+        return oid
+
+    def cone(self, minimum=-math.inf, maximum=math.inf, closed=False, transform=None, material=None, pattern=-1,
+             parent=-1):
+        return self.cylinder(minimum, maximum, closed, transform, material, pattern, parent, cone=True)
+
+    def csg(self, op, transform=None, parent=-1):
+        """CSG node; add its left then its right child with parent=<this id> (csg.rs:51-65)."""
+        oid = self._obj(_lib.CSG, parent, transform, None, -1)
+        self.csg_op[oid] = _lib.CSG_OPS[op] if isinstance(op, str) else int(op)
+        return oid
 
     def triangle(self, p1, p2, p3, transform=None, material=None, pattern=-1, parent=-1):
         return self._obj(_lib.TRIANGLE, parent, transform, material, pattern, list(p1) + list(p2) + list(p3) + [0.0] * 9)
@@ -118,6 +141,7 @@ class SceneBuilder:
             "light_kind": np.array(self.light_kind or [0], np.int32),
             "light": np.array(self.light or [0.0], np.float64),
             "light_level": np.array(self.light_level or [0], np.int32),
+            "shape": np.array(self.shape or [0.0], np.float64), "csg_op": np.array(self.csg_op or [0], np.int32),
         }
         d = _lib.SceneDesc()
         d.n_objects = len(self.kind)

@@ -59,7 +59,8 @@ def _inspect(R, desc):
 YAMLS = [(SCENES, f) for f in ("c1_readme.yaml", "c2_s1024.yaml", "c3_s1024_reflect.yaml", "c4_teapot.yaml",
                                "c5_area_light.yaml")] + \
         [(GOLDEN, f) for f in ("checker_pattern.yaml", "stripe_pattern.yaml", "gradient_pattern.yaml",
-                               "ring_pattern.yaml", "blend_pattern.yaml", "triangle.yaml")]
+                               "ring_pattern.yaml", "blend_pattern.yaml", "triangle.yaml", "objects_cylinder.yaml",
+                               "objects_cone.yaml", "shapes_csg.yaml", "shapes_glass.yaml", "shapes_mixed.yaml")]
 
 
 @pytest.mark.parametrize("root,name", YAMLS)
@@ -77,8 +78,12 @@ def test_yaml_front_end_matches_oracle_builder(R, oracle_mod, root, name):
     for i in range(d.n_objects):
         ref = np.array(o.inverse_of(i)).reshape(4, 4)
         assert np.array_equal(inv[i].reshape(4, 4)[:3], ref[:3]), (name, i)
-        if d.kind[i] == 2:
+        if d.kind[i] in (2, 8):  # group, CSG: cached AABB (group.rs:128-149, csg.rs get_aabb)
             assert np.array_equal(aabb[i], np.array(o.group_aabb(i)), equal_nan=True), (name, i)
+        if d.kind[i] in (6, 7):  # cylinder / cone parameters
+            assert [d.shape[3 * i + k] for k in range(3)] == o.shape_params(i), (name, i)
+        if d.kind[i] == 8:
+            assert d.csg_op[i] == o.csg_op(i), (name, i)
     for f in ("hsize", "vsize", "pixel_size", "half_width", "half_height"):
         assert getattr(s.camera, f) == getattr(cam, f), f
     assert list(s.camera.transform) == list(cam.transform)
@@ -100,8 +105,8 @@ def test_yaml_edge_cases(R):
         R.YamlScene(base + "lights:\r  - type: spot\r    color: [1,1,1]\rscene: []\r", 10, 10, 1)
     with pytest.raises(R.RRError) as e:
         R.YamlScene(base + "lights:\r  - type: point\r    color: [1,1,1]\r    position: [0,0,0]\r"
-                    "scene:\r  - type: cube\r", 10, 10, 1)
-    assert e.value.code == -5  # RR_E_LIMIT: out-of-scope shape, reported not silently dropped
+                    "scene:\r  - type: torus\r    minor_radius: 0.25\r", 10, 10, 1)
+    assert e.value.code == -5  # RR_E_LIMIT: out-of-scope shape (next-4), reported not silently dropped
 
 
 def test_obj_loader_counts(R):
@@ -148,3 +153,25 @@ def test_camera_new_matches_oracle(R, oracle_mod):
 def test_jitter_is_deterministic_and_uniform(oracle_mod):
     v = np.array([oracle_mod.Oracle.jitter(0, s, 1, 0, k, 0) for s in range(200) for k in range(25)])
     assert v.min() >= 0 and v.max() < 1 and abs(v.mean() - 0.5) < 0.02
+
+
+def test_shape_and_csg_descriptor_checks(R):
+    """A CSG needs a left and a right child (csg.rs panics on get_object(usize::MAX)); CSG subtrees
+    are bounded by RR_MAX_CSG_ENTRIES intersections per ray."""
+    b = R.SceneBuilder()
+    b.point_light((-10, 10, -10), (1, 1, 1))
+    c = b.csg("union")
+    b.sphere(parent=c)
+    with pytest.raises(R.RRError) as e:
+        _inspect(R, b.desc())
+    assert e.value.code == R._lib.RR_E_SCENE
+    b = R.SceneBuilder()
+    b.point_light((-10, 10, -10), (1, 1, 1))
+    c = b.csg("union")
+    g = b.group(parent=c)
+    for _ in range(9):
+        b.cylinder(-1, 1, True, parent=g)
+    b.sphere(parent=c)
+    with pytest.raises(R.RRError) as e:
+        _inspect(R, b.desc())
+    assert e.value.code == R._lib.RR_E_LIMIT

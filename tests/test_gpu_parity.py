@@ -101,6 +101,40 @@ def test_reference_example_scenes(renderer, name):
     _compare(got["avg"], o.aa_average(canvas, 1), name)
 
 
+@pytest.mark.parametrize("name,W,H,aa", [("shapes_csg.yaml", 64, 32, 2), ("shapes_glass.yaml", 64, 32, 2),
+                                         ("shapes_mixed.yaml", 64, 32, 2), ("objects_cylinder.yaml", 48, 24, 1),
+                                         ("objects_cone.yaml", 48, 24, 1)])
+def test_shape_scenes(renderer, name, W, H, aa):
+    """Cube / cylinder / cone / CSG through the general kernel variant: 4-entry
+    leaves, CSG subtrees evaluated per lane, n1/n2 over filtered entries."""
+    scene, (o, cam) = _yaml_pair(name, W, H, aa, obj_root=GOLDEN, path=os.path.join(GOLDEN, name))
+    renderer.upload(scene)
+    got = renderer.render(scene.camera, aa=aa, max_depth=5, canvas=True)
+    canvas, st = o.render(cam, max_depth=5)
+    _compare(got["canvas"], canvas, name + " canvas")
+    _compare(got["avg"], o.aa_average(canvas, aa), name + " avg")
+    assert got["stats"]["rays"] == st["rays"] - st["shadow_rays"]
+    assert got["stats"]["shadow_rays"] == st["shadow_rays"]
+    assert got["stats"]["shade_events"] == st["shade_events"]
+
+
+@pytest.mark.parametrize("name,png", [("objects_cylinder.yaml", "objects_cylinder.png"),
+                                      ("objects_cone.yaml", "objects_cone.png")])
+def test_reference_png_through_gpu(renderer, R, name, png):
+    """The reference renderer's own 800x400 aa=3 outputs (examples/objects/*.png), reproduced by the
+    GPU path through quantisation (canvas.rs:76-105)."""
+    PIL = pytest.importorskip("PIL.Image")
+    text = open(os.path.join(GOLDEN, name)).read()
+    scene = R.YamlScene(text, 800, 400, 3, obj_root=GOLDEN)
+    renderer.upload(scene)
+    avg = renderer.render(scene.camera, aa=3, max_depth=5)["avg"]
+    q = R.quantize(avg)[..., :3]
+    ref = np.asarray(PIL.open(os.path.join(GOLDEN, "png", png)).convert("RGB"))
+    diff = int((q != ref).any(axis=2).sum())
+    print(f"{png}: {diff} of {ref.shape[0] * ref.shape[1]} pixels differ")
+    assert diff == 0
+
+
 def test_multi_part_tiles_are_bit_identical(renderer, R):
     """Row-interleaved tiles (the multi-GPU partition) reassemble to the 1-part image bit-for-bit."""
     scene, _ = _yaml_pair("c3_s1024_reflect.yaml", 48, 40, 1)
