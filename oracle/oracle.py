@@ -90,6 +90,11 @@ def _load():
         L.orc_set_shape_params.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_int]
         L.orc_set_csg_op.argtypes = [C.c_void_p, C.c_int, C.c_int]
         L.orc_csg_allowed.argtypes = [C.c_int] * 4
+        L.orc_pattern_set_noise.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_double]
+        L.orc_noise_3d.argtypes = [C.c_double] * 3
+        L.orc_noise_3d.restype = C.c_double
+        L.orc_octave_perlin.argtypes = [C.c_double] * 3 + [C.c_int64, C.c_double]
+        L.orc_octave_perlin.restype = C.c_double
         L.orc_get_shape_params.argtypes = [C.c_void_p, C.c_int, _D]
         L.orc_get_csg_op.argtypes = [C.c_void_p, C.c_int]
         L.orc_csg_filter.argtypes = [C.c_void_p, C.c_int, C.c_int, _D, _I, _I]
@@ -183,7 +188,8 @@ class Mat:
 
 DEFAULT_MAT7 = (0.1, 0.9, 0.9, 200.0, 0.0, 0.0, 1.0)  # material.rs:47-58
 
-PAT = {"test": 0, "solid": 1, "stripe": 2, "gradient": 3, "ring": 4, "checker": 5, "blend": 6}
+PAT = {"test": 0, "solid": 1, "stripe": 2, "gradient": 3, "ring": 4, "checker": 5, "blend": 6, "perturbed": 7,
+       "noise": 8}
 KIND = {"sphere": 0, "plane": 1, "group": 2, "triangle": 3, "smooth_triangle": 4, "cube": 5, "cylinder": 6,
         "cone": 7, "csg": 8}
 CSG_OP = {"union": 0, "intersection": 1, "difference": 2}  # csg.rs:13-17
@@ -266,6 +272,9 @@ class Oracle:
         k = PAT[kind] if isinstance(kind, str) else kind
         return self.L.orc_pattern_new(self.w, k, _dv(color) if color is not None else None, a, b, float(scale),
                                       _dv(transform) if transform is not None else None)
+
+    def set_noise(self, pid, octaves, persistence):
+        self.L.orc_pattern_set_noise(self.w, pid, int(octaves), float(persistence))
 
     def point_light(self, pos, color):
         return self.L.orc_add_point_light(self.w, _dv(pos), _dv(color))

@@ -219,6 +219,8 @@ struct Pattern {
     Color color = {1.0, 1.0, 1.0};
     int a = -1, b = -1;
     double scale = 0.5;
+    int64_t octaves = 0;       // perturbed / noise (usize)
+    double persistence = 0.0;
     Matrix transform = identity4();
     Matrix inv = identity4();
 };
@@ -705,6 +707,74 @@ int32_t sat_i32(double v) {
 }
 
 // pattern.rs:145-215
+// ---------------------------------------------------------------- noise.rs
+// fastnoise-lite 1.1.1 (crate feature "f64"), NoiseType::Perlin with the defaults noise.rs keeps:
+// seed 1337, frequency 0.01 (an f32, widened to f64 when the coordinates are scaled), no fractal,
+// no domain rotation.  Lattice coordinates are f64 (FastFloor), the fractional parts are cast to
+// f32 and everything after is f32 arithmetic; get_noise_3d returns the f32 noise.
+namespace fnl {
+const int32_t PRIME_X = 501125321, PRIME_Y = 1136930381, PRIME_Z = 1720413743;
+const float GRADIENTS_3D[256] = {
+    0, 1, 1, 0, 0, -1, 1, 0, 0, 1, -1, 0, 0, -1, -1, 0, 1, 0, 1, 0, -1, 0, 1, 0, 1, 0, -1, 0, -1, 0, -1, 0,
+    1, 1, 0, 0, -1, 1, 0, 0, 1, -1, 0, 0, -1, -1, 0, 0, 0, 1, 1, 0, 0, -1, 1, 0, 0, 1, -1, 0, 0, -1, -1, 0,
+    1, 0, 1, 0, -1, 0, 1, 0, 1, 0, -1, 0, -1, 0, -1, 0, 1, 1, 0, 0, -1, 1, 0, 0, 1, -1, 0, 0, -1, -1, 0, 0,
+    0, 1, 1, 0, 0, -1, 1, 0, 0, 1, -1, 0, 0, -1, -1, 0, 1, 0, 1, 0, -1, 0, 1, 0, 1, 0, -1, 0, -1, 0, -1, 0,
+    1, 1, 0, 0, -1, 1, 0, 0, 1, -1, 0, 0, -1, -1, 0, 0, 0, 1, 1, 0, 0, -1, 1, 0, 0, 1, -1, 0, 0, -1, -1, 0,
+    1, 0, 1, 0, -1, 0, 1, 0, 1, 0, -1, 0, -1, 0, -1, 0, 1, 1, 0, 0, -1, 1, 0, 0, 1, -1, 0, 0, -1, -1, 0, 0,
+    0, 1, 1, 0, 0, -1, 1, 0, 0, 1, -1, 0, 0, -1, -1, 0, 1, 0, 1, 0, -1, 0, 1, 0, 1, 0, -1, 0, -1, 0, -1, 0,
+    1, 1, 0, 0, -1, 1, 0, 0, 1, -1, 0, 0, -1, -1, 0, 0, 1, 1, 0, 0, 0, -1, 1, 0, -1, 1, 0, 0, 0, -1, -1, 0};
+int32_t as_i32(double f) {  // Rust `as i32`: truncate, saturate, NaN -> 0
+    if (f != f) return 0;
+    if (f >= 2147483647.0) return 2147483647;
+    if (f <= -2147483648.0) return INT32_MIN;
+    return (int32_t)f;
+}
+int32_t fast_floor(double f) { return f >= 0 ? as_i32(f) : (int32_t)((uint32_t)as_i32(f) - 1u); }
+int32_t wmul(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+int32_t wadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+float interp_quintic(float t) { return t * t * t * (t * (t * 6.0f - 15.0f) + 10.0f); }
+float lerp(float a, float b, float t) { return a + t * (b - a); }
+float grad_coord(int32_t seed, int32_t xp, int32_t yp, int32_t zp, float xd, float yd, float zd) {
+    int32_t hash = wmul(seed ^ xp ^ yp ^ zp, 0x27d4eb2d);
+    hash ^= hash >> 15;  // arithmetic shift (i32)
+    hash &= 63 << 2;
+    return xd * GRADIENTS_3D[hash] + yd * GRADIENTS_3D[hash | 1] + zd * GRADIENTS_3D[hash | 2];
+}
+float single_perlin(int32_t seed, double x, double y, double z) {
+    int32_t x0 = fast_floor(x), y0 = fast_floor(y), z0 = fast_floor(z);
+    float xd0 = (float)(x - (double)x0), yd0 = (float)(y - (double)y0), zd0 = (float)(z - (double)z0);
+    float xd1 = xd0 - 1.0f, yd1 = yd0 - 1.0f, zd1 = zd0 - 1.0f;
+    float xs = interp_quintic(xd0), ys = interp_quintic(yd0), zs = interp_quintic(zd0);
+    x0 = wmul(x0, PRIME_X);
+    y0 = wmul(y0, PRIME_Y);
+    z0 = wmul(z0, PRIME_Z);
+    int32_t x1 = wadd(x0, PRIME_X), y1 = wadd(y0, PRIME_Y), z1 = wadd(z0, PRIME_Z);
+    float xf00 = lerp(grad_coord(seed, x0, y0, z0, xd0, yd0, zd0), grad_coord(seed, x1, y0, z0, xd1, yd0, zd0), xs);
+    float xf10 = lerp(grad_coord(seed, x0, y1, z0, xd0, yd1, zd0), grad_coord(seed, x1, y1, z0, xd1, yd1, zd0), xs);
+    float xf01 = lerp(grad_coord(seed, x0, y0, z1, xd0, yd0, zd1), grad_coord(seed, x1, y0, z1, xd1, yd0, zd1), xs);
+    float xf11 = lerp(grad_coord(seed, x0, y1, z1, xd0, yd1, zd1), grad_coord(seed, x1, y1, z1, xd1, yd1, zd1), xs);
+    float yf0 = lerp(xf00, xf10, ys);
+    float yf1 = lerp(xf01, xf11, ys);
+    return lerp(yf0, yf1, zs) * 0.964921414852142333984375f;
+}
+float get_noise_3d(double x, double y, double z) {
+    const double freq = (double)0.01f;  // frequency: f32, `as Float` when scaling the coordinates
+    return single_perlin(1337, x * freq, y * freq, z * freq);
+}
+}  // namespace fnl
+
+// noise.rs:11-29
+double octave_perlin(double x, double y, double z, int64_t octaves, double persistence) {
+    double total = 0.0, frequency = 1.0, amplitude = 1.0, max_value = 0.0;
+    for (int64_t i = 0; i < octaves; ++i) {
+        total += (double)fnl::get_noise_3d(x * frequency, y * frequency, z * frequency) * amplitude;
+        max_value += amplitude;
+        amplitude *= persistence;
+        frequency *= 2.0;
+    }
+    return total / max_value;
+}
+
 Color pattern_at(const orc_world* w, int pidx, const Tuple& object_point) {
     const Pattern& p = pat(w, pidx);
     Tuple pp = mul_tuple(p.inv, object_point);
@@ -730,6 +800,19 @@ Color pattern_at(const orc_world* w, int pidx, const Tuple& object_point) {
             Color a = pattern_at(w, p.a, pp);
             Color b = pattern_at(w, p.b, pp);
             return cadd(cmul(a, 1.0 - p.scale), cmul(b, p.scale));
+        }
+        case ORC_PAT_PERTURBED: {  // pattern.rs:187-199
+            double nx = octave_perlin(pp.x, pp.y, pp.z, p.octaves, p.persistence) * p.scale;
+            double ny = octave_perlin(pp.x, pp.y, pp.z + 1.0, p.octaves, p.persistence) * p.scale;
+            double nz = octave_perlin(pp.x, pp.y, pp.z + 2.0, p.octaves, p.persistence) * p.scale;
+            Tuple np = {pp.x + nx, pp.y + ny, pp.z + nz, pp.w};
+            return pattern_at(w, p.a, np);
+        }
+        case ORC_PAT_NOISE: {  // pattern.rs:200-208
+            double n = octave_perlin(pp.x, pp.y, pp.z, p.octaves, p.persistence);
+            n = n * p.scale;
+            if (n <= 0.0) return cmul(pattern_at(w, p.a, pp), -n);
+            return cmul(pattern_at(w, p.b, pp), n);
         }
     }
     return BLACK;
@@ -1026,6 +1109,14 @@ int orc_pattern_new(orc_world* w, int kind, const double color[3], int a, int b,
     p.inv = inverse(p.transform);
     w->patterns.push_back(p);
     return (int)w->patterns.size() - 1;
+}
+void orc_pattern_set_noise(orc_world* w, int pattern, int64_t octaves, double persistence) {
+    w->patterns[pattern].octaves = octaves;
+    w->patterns[pattern].persistence = persistence;
+}
+double orc_noise_3d(double x, double y, double z) { return (double)fnl::get_noise_3d(x, y, z); }
+double orc_octave_perlin(double x, double y, double z, int64_t octaves, double persistence) {
+    return octave_perlin(x, y, z, octaves, persistence);
 }
 int orc_add_point_light(orc_world* w, const double pos[3], const double color[3]) {
     Light l;

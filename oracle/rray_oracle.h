@@ -29,7 +29,7 @@ typedef struct orc_world orc_world;
 
 /* pattern kinds (pattern.rs:10-21) */
 enum { ORC_PAT_TEST = 0, ORC_PAT_SOLID = 1, ORC_PAT_STRIPE = 2, ORC_PAT_GRADIENT = 3,
-       ORC_PAT_RING = 4, ORC_PAT_CHECKER = 5, ORC_PAT_BLEND = 6 };
+       ORC_PAT_RING = 4, ORC_PAT_CHECKER = 5, ORC_PAT_BLEND = 6, ORC_PAT_PERTURBED = 7, ORC_PAT_NOISE = 8 };
 /* object kinds */
 enum { ORC_SPHERE = 0, ORC_PLANE = 1, ORC_GROUP = 2, ORC_TRIANGLE = 3, ORC_SMOOTH_TRIANGLE = 4,
        ORC_CUBE = 5, ORC_CYLINDER = 6, ORC_CONE = 7, ORC_CSG = 8 };
@@ -79,6 +79,11 @@ int  orc_csg_filter(orc_world* w, int csg, int n, const double* t, const int* ob
 /* mat7 = ambient, diffuse, specular, shininess, reflective, transparency, refractive_index */
 void orc_set_material(orc_world* w, int id, const double mat7[7], int pattern /* -1 = default white solid */);
 int  orc_pattern_new(orc_world* w, int kind, const double color[3], int a, int b, double scale, const double m[16]);
+/* perturbed / noise: octaves and persistence (pattern.rs:104-118; scale is the pattern's scale) */
+void orc_pattern_set_noise(orc_world* w, int pattern, int64_t octaves, double persistence);
+/* noise.rs: fastnoise-lite 1.1.1 Perlin (seed 1337, frequency 0.01f) and octave_perlin */
+double orc_noise_3d(double x, double y, double z);
+double orc_octave_perlin(double x, double y, double z, int64_t octaves, double persistence);
 int  orc_add_point_light(orc_world* w, const double pos[3], const double color[3]);
 int  orc_add_area_light(orc_world* w, const double corner[3], const double u[3], const double v[3],
                         const double color[3], int level);

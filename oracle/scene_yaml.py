@@ -86,6 +86,12 @@ def get_f64_default(node, default):  # :76-82
     return float(node)
 
 
+def _as_usize(v):  # Rust `f64 as usize`: truncate, saturate at 0, NaN -> 0
+    if v != v or v <= 0:
+        return 0
+    return int(min(v, 2.0 ** 63))
+
+
 def deg2rad(d):  # :25-27
     return d * math.pi / 180.0
 
@@ -141,8 +147,25 @@ class YamlSceneBuilder:
             b = self.sub_pattern(transform, _get(p, "color_b"), _get(p, "pattern_b"))
             scale = get_f64_default(_get(p, "scale"), 0.5) if ty == "blend" else 0.5
             return self.o.pattern(ty, a=a, b=b, scale=scale, transform=transform)
-        if ty in ("perturbed", "noise", "image"):
-            raise NotImplementedError(f"pattern '{ty}' is out of scope (SURVEY.md §2)")
+        if ty == "perturbed":  # :272-281
+            scale = get_f64_default(_get(p, "scale"), 0.2)
+            octaves = _as_usize(get_f64_default(_get(p, "octaves"), 3.0))
+            persistence = get_f64_default(_get(p, "persistence"), 0.5)
+            a = self.sub_pattern(transform, _get(p, "color_a"), _get(p, "pattern_a"))
+            pid = self.o.pattern("perturbed", a=a, scale=scale, transform=transform)
+            self.o.set_noise(pid, octaves, persistence)
+            return pid
+        if ty == "noise":  # :282-292
+            octaves = _as_usize(get_f64_default(_get(p, "octaves"), 1.0))
+            persistence = get_f64_default(_get(p, "persistence"), 1.0)
+            scale = get_f64_default(_get(p, "scale"), 1.0)
+            a = self.sub_pattern(transform, _get(p, "color_a"), _get(p, "pattern_a"))
+            b = self.sub_pattern(transform, _get(p, "color_b"), _get(p, "pattern_b"))
+            pid = self.o.pattern("noise", a=a, b=b, scale=scale, transform=transform)
+            self.o.set_noise(pid, octaves, persistence)
+            return pid
+        if ty == "image":
+            raise NotImplementedError("pattern 'image' is out of scope (SURVEY.md §8 next-3: texture)")
         return self.o.pattern("solid", color=(0.0, 0.0, 0.0), transform=transform)
 
     def sub_pattern(self, transform, color, pat):  # :310-317

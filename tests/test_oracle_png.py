@@ -3,7 +3,9 @@
 rendered by the Rust binary at 800x400.  The oracle renders the same YAML, box-averages and
 quantises (`as u8`, canvas.rs:76-105), and must reproduce every pixel.  The pattern scenes were
 rendered with aa=1, the objects scenes with aa=3 (every other aa leaves ~7 % of the edge pixels
-different; aa=3 leaves none).  Scenes with noise / texture patterns or torus are next-3/next-4."""
+different; aa=3 leaves none).  noise_pattern / perturbed_pattern and objects/sphere, objects/cube
+(blends of noise patterns) pin the fastnoise-lite 1.1.1 Perlin restatement (oracle/rray_oracle.cpp,
+namespace fnl) and noise.rs:octave_perlin.  Texture (image / uv) patterns and torus are next."""
 import os
 
 import numpy as np
@@ -15,7 +17,9 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 CASES = [("checker_pattern.yaml", "checker_pattern.png", 1), ("stripe_pattern.yaml", "stripe_pattern.png", 1),
          ("ring_pattern.yaml", "ring_pattern.png", 1), ("gradient_pattern.yaml", "gradient_pattern.png", 1),
          ("blend_pattern.yaml", "blend_pattern.png", 1), ("triangle.yaml", "triangle.png", 3),
-         ("objects_cylinder.yaml", "objects_cylinder.png", 3), ("objects_cone.yaml", "objects_cone.png", 3)]
+         ("objects_cylinder.yaml", "objects_cylinder.png", 3), ("objects_cone.yaml", "objects_cone.png", 3),
+         ("noise_pattern.yaml", "noise_pattern.png", 1), ("perturbed_pattern.yaml", "perturbed_pattern.png", 1),
+         ("objects_sphere.yaml", "objects_sphere.png", 3), ("objects_cube.yaml", "objects_cube.png", 3)]
 
 
 def _png_rgb(path):
