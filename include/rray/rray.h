@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 3
+#define RR_ABI_VERSION 4
 
 /* error codes */
 #define RR_OK 0
@@ -46,7 +46,7 @@ enum { RR_SPHERE = 0, RR_PLANE = 1, RR_GROUP = 2, RR_TRIANGLE = 3, RR_SMOOTH_TRI
 enum { RR_CSG_UNION = 0, RR_CSG_INTERSECTION = 1, RR_CSG_DIFFERENCE = 2 };
 /* pattern kinds — PatternType (src/raytracer/material/pattern.rs:10-21), in-scope subset */
 enum { RR_PAT_TEST = 0, RR_PAT_SOLID = 1, RR_PAT_STRIPE = 2, RR_PAT_GRADIENT = 3,
-       RR_PAT_RING = 4, RR_PAT_CHECKER = 5, RR_PAT_BLEND = 6 };
+       RR_PAT_RING = 4, RR_PAT_CHECKER = 5, RR_PAT_BLEND = 6, RR_PAT_PERTURBED = 7, RR_PAT_NOISE = 8 };
 /* light kinds — LightType (src/raytracer/light.rs:10-14) */
 enum { RR_LIGHT_POINT = 0, RR_LIGHT_AREA = 1 };
 
@@ -54,6 +54,7 @@ enum { RR_LIGHT_POINT = 0, RR_LIGHT_AREA = 1 };
 #define RR_MAX_GROUP_DEPTH 6    /* nested group levels */
 #define RR_MAX_PATTERN_DEPTH 8  /* nested pattern levels */
 #define RR_MAX_CSG_ENTRIES 32   /* intersections one CSG subtree can produce for one ray */
+#define RR_MAX_OCTAVES 64       /* octave_perlin octaves (noise.rs:11-29) */
 
 /*
  * The scene exactly as the reference's object registry holds it (object/db.rs:11-13 +
@@ -97,6 +98,10 @@ typedef struct {
                                     cone.rs:30-38); NULL: -inf, +inf, open */
     const int32_t* csg_op;       /* optional per object: RR_CSG_* (CSG objects; their two children,
                                     left then right, are the group child lists) */
+    /* ABI 4: Perturbed / Noise patterns (pattern.rs:16-19); pat_scale is their scale, pat_a the
+       perturbed pattern, pat_a / pat_b the noise's two sub-patterns */
+    const int32_t* pat_octaves;      /* optional per pattern (`usize`, <= RR_MAX_OCTAVES); NULL: 1 */
+    const double* pat_persistence;   /* optional per pattern; NULL: 1.0 */
 } rr_scene_desc;
 
 /* Camera (camera.rs:18-27): hsize/vsize are the SUPERSAMPLED sizes (W*aa, H*aa). */

@@ -64,6 +64,9 @@ def _load():
         L.orc_remove_light.argtypes = [C.c_void_p, C.c_int]
         L.orc_num_children.argtypes = [C.c_void_p, C.c_int]
         L.orc_num_objects.argtypes = [C.c_void_p]
+        L.orc_num_patterns.argtypes = [C.c_void_p]
+        L.orc_pattern_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_double),
+                                       C.POINTER(C.c_int64)]
         L.orc_get_inverse.argtypes = [C.c_void_p, C.c_int, _D]
         L.orc_intersect.argtypes = [C.c_void_p, _D, _D, C.c_int, _D, _I, _D, _D]
         L.orc_local_intersect.argtypes = [C.c_void_p, C.c_int, _D, _D, C.c_int, _D, _I, _D, _D]
@@ -290,6 +293,15 @@ class Oracle:
 
     def num_objects(self):
         return self.L.orc_num_objects(self.w)
+
+    def num_patterns(self):
+        return self.L.orc_num_patterns(self.w)
+
+    def pattern_info(self, pid):
+        """(kind, a, b, scale, octaves, persistence) of one pattern tree node."""
+        ints, dbl, octv = (C.c_int32 * 3)(), (C.c_double * 2)(), C.c_int64()
+        self.L.orc_pattern_info(self.w, pid, ints, dbl, C.byref(octv))
+        return ints[0], ints[1], ints[2], dbl[0], octv.value, dbl[1]
 
     def inverse_of(self, oid):
         o = _out(16)

@@ -1142,6 +1142,16 @@ int orc_add_area_light(orc_world* w, const double corner[3], const double u[3], 
 void orc_remove_light(orc_world* w, int index) { w->lights.erase(w->lights.begin() + index); }
 int orc_num_children(orc_world* w, int id) { return (int)w->objects[id].children.size(); }
 int orc_num_objects(orc_world* w) { return (int)w->objects.size(); }
+int orc_num_patterns(orc_world* w) { return (int)w->patterns.size(); }
+void orc_pattern_info(orc_world* w, int id, int32_t ints[3], double dbl[2], int64_t* octaves) {
+    const Pattern& p = w->patterns[id];
+    ints[0] = p.kind;
+    ints[1] = p.a;
+    ints[2] = p.b;
+    dbl[0] = p.scale;
+    dbl[1] = p.persistence;
+    *octaves = p.octaves;
+}
 void orc_get_inverse(orc_world* w, int id, double out[16]) { to16(w->objects[id].inv, out); }
 
 void orc_set_context(orc_world* w, uint64_t seed, int jitter_mode, uint64_t sample) {

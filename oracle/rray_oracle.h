@@ -90,6 +90,9 @@ int  orc_add_area_light(orc_world* w, const double corner[3], const double u[3],
 void orc_remove_light(orc_world* w, int index);
 int  orc_num_children(orc_world* w, int id);
 int  orc_num_objects(orc_world* w);
+int  orc_num_patterns(orc_world* w);
+/* kind, a, b -> ints[3]; scale, persistence -> dbl[2]; octaves -> *octaves */
+void orc_pattern_info(orc_world* w, int id, int32_t ints[3], double dbl[2], int64_t* octaves);
 void orc_get_inverse(orc_world* w, int id, double out[16]);
 
 /* ---- queries mirroring the reference's unit-test entry points ---- */

@@ -18,7 +18,8 @@ globals().update({name: code for code, name in ERRORS.items()})  # RR_E_ARG = -1
 RR_OUT_CANVAS, RR_OUT_AVG, RR_OUT_AVG_F32 = 1, 2, 4
 SPHERE, PLANE, GROUP, TRIANGLE, SMOOTH_TRIANGLE, CUBE, CYLINDER, CONE, CSG = range(9)
 CSG_OPS = {"union": 0, "intersection": 1, "difference": 2}
-PAT = {"test": 0, "solid": 1, "stripe": 2, "gradient": 3, "ring": 4, "checker": 5, "blend": 6}
+PAT = {"test": 0, "solid": 1, "stripe": 2, "gradient": 3, "ring": 4, "checker": 5, "blend": 6, "perturbed": 7,
+       "noise": 8}
 LIGHT_POINT, LIGHT_AREA = 0, 1
 KERNELS = ["trace", "n1n2", "shade", "shadow", "finish", "combine", "aa", "trace_shade"]
 
@@ -32,7 +33,8 @@ class SceneDesc(C.Structure):
                 ("n_top", C.c_int32), ("top", _I), ("n_materials", C.c_int32), ("mat", _D), ("mat_pattern", _I),
                 ("n_patterns", C.c_int32), ("pat_kind", _I), ("pat_a", _I), ("pat_b", _I), ("pat_color", _D),
                 ("pat_scale", _D), ("pat_transform", _D), ("n_lights", C.c_int32), ("light_kind", _I),
-                ("light", _D), ("light_level", _I), ("shape", _D), ("csg_op", _I)]
+                ("light", _D), ("light_level", _I), ("shape", _D), ("csg_op", _I), ("pat_octaves", _I),
+                ("pat_persistence", _D)]
 
 
 class Camera(C.Structure):

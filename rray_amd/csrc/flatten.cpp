@@ -281,15 +281,22 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
         p.b = d.pat_b ? d.pat_b[i] : -1;
         for (int c = 0; c < 3; ++c) p.color[c] = d.pat_color ? d.pat_color[3 * (size_t)i + c] : 0.0;
         p.scale = d.pat_scale ? d.pat_scale[i] : 0.5;
+        p.octaves = d.pat_octaves ? d.pat_octaves[i] : 1;
+        p.persistence = d.pat_persistence ? d.pat_persistence[i] : 1.0;
         M4 t = d.pat_transform ? load16(d.pat_transform + 16 * (size_t)i) : identity();
         if (!inverse_3x4(t, nullptr, p.inv, nullptr, err)) return RR_E_NONAFFINE;
         p.flags = is_identity12(p.inv) ? NF_IDENT : 0;
-        if (p.kind < RR_PAT_TEST || p.kind > RR_PAT_BLEND) {
+        if (p.kind < RR_PAT_TEST || p.kind > RR_PAT_NOISE) {
             err = "unknown pattern kind";
             return RR_E_ARG;
         }
-        bool binary = p.kind != RR_PAT_TEST && p.kind != RR_PAT_SOLID;
-        if (binary && (p.a < 0 || p.a >= d.n_patterns || p.b < 0 || p.b >= d.n_patterns)) {
+        if ((p.kind == RR_PAT_PERTURBED || p.kind == RR_PAT_NOISE) && (p.octaves < 0 || p.octaves > RR_MAX_OCTAVES)) {
+            err = "pattern octaves outside [0, RR_MAX_OCTAVES]";
+            return RR_E_LIMIT;
+        }
+        bool leaf = p.kind == RR_PAT_TEST || p.kind == RR_PAT_SOLID;
+        bool unary = p.kind == RR_PAT_PERTURBED;
+        if (!leaf && (p.a < 0 || p.a >= d.n_patterns || (!unary && (p.b < 0 || p.b >= d.n_patterns)))) {
             err = "pattern child index out of range";
             return RR_E_ARG;
         }
@@ -300,6 +307,7 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
         if (lvl > RR_MAX_PATTERN_DEPTH) return lvl;
         const DevPattern& p = out.pats[i];
         if (p.kind == RR_PAT_TEST || p.kind == RR_PAT_SOLID) return lvl;
+        if (p.kind == RR_PAT_PERTURBED) return pdepth(p.a, lvl + 1);
         return std::max(pdepth(p.a, lvl + 1), pdepth(p.b, lvl + 1));
     };
     for (int i = 0; i < d.n_patterns; ++i)

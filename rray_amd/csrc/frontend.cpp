@@ -29,6 +29,8 @@ struct rr_scene {
     std::vector<int32_t> mat_pattern;
     std::vector<int32_t> pat_kind, pat_a, pat_b;
     std::vector<double> pat_color, pat_scale, pat_transform;
+    std::vector<int32_t> pat_octaves;
+    std::vector<double> pat_persistence;
     std::vector<int32_t> light_kind, light_level;
     std::vector<double> light;
     std::vector<double> shape;      // minimum, maximum, closed per object (cylinder / cone)
@@ -73,6 +75,8 @@ struct rr_scene {
         desc.light_level = light_level.data();
         desc.shape = shape.data();
         desc.csg_op = csg_op.data();
+        desc.pat_octaves = pat_octaves.data();
+        desc.pat_persistence = pat_persistence.data();
     }
 };
 
@@ -144,13 +148,15 @@ struct Builder {
     std::string obj_root;
 
     int add_pattern(int kind, const rr::M4& m, double r = 0, double g = 0, double b = 0, int a = -1, int bb = -1,
-                    double scale = 0.5) {
+                    double scale = 0.5, int32_t octaves = 1, double persistence = 1.0) {
         S.pat_kind.push_back(kind);
         S.pat_a.push_back(a);
         S.pat_b.push_back(bb);
         S.pat_color.insert(S.pat_color.end(), {r, g, b});
         S.pat_scale.push_back(scale);
         S.pat_transform.insert(S.pat_transform.end(), m.m, m.m + 16);
+        S.pat_octaves.push_back(octaves);
+        S.pat_persistence.push_back(persistence);
         return (int)S.pat_kind.size() - 1;
     }
     int create_pattern(const Node& p) {  // :226-308
@@ -172,9 +178,29 @@ struct Builder {
             int b = sub_pattern(transform, p["color_b"], p["pattern_b"]);
             return add_pattern(kind, transform, 0, 0, 0, a, b, scale);
         }
-        if (ty.s == "perturbed" || ty.s == "noise" || ty.s == "image")
-            panic("pattern '" + ty.s + "' is outside the GPU path's scope (SURVEY.md §2)", RR_E_LIMIT);
+        if (ty.s == "perturbed") {  // :272-281
+            double scale = get_f64_default(p["scale"], 0.2);
+            int32_t octaves = as_octaves(get_f64_default(p["octaves"], 3.0));
+            double persistence = get_f64_default(p["persistence"], 0.5);
+            int a = sub_pattern(transform, p["color_a"], p["pattern_a"]);
+            return add_pattern(RR_PAT_PERTURBED, transform, 0, 0, 0, a, -1, scale, octaves, persistence);
+        }
+        if (ty.s == "noise") {  // :282-292
+            int32_t octaves = as_octaves(get_f64_default(p["octaves"], 1.0));
+            double persistence = get_f64_default(p["persistence"], 1.0);
+            double scale = get_f64_default(p["scale"], 1.0);
+            int a = sub_pattern(transform, p["color_a"], p["pattern_a"]);
+            int b = sub_pattern(transform, p["color_b"], p["pattern_b"]);
+            return add_pattern(RR_PAT_NOISE, transform, 0, 0, 0, a, b, scale, octaves, persistence);
+        }
+        if (ty.s == "image")
+            panic("pattern 'image' is outside the GPU path's scope (SURVEY.md §8 next-3: texture)", RR_E_LIMIT);
         return add_pattern(RR_PAT_SOLID, transform, 0, 0, 0);
+    }
+    // `f64 as usize` (saturating, NaN -> 0); counts above RR_MAX_OCTAVES are rejected at upload
+    static int32_t as_octaves(double v) {
+        if (!(v > 0)) return 0;
+        return v >= 2147483647.0 ? 2147483647 : (int32_t)v;
     }
     int sub_pattern(const rr::M4& t, const Node& color, const Node& pat) {  // :310-317
         if (color.is_array()) {

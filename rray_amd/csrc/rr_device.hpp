@@ -71,6 +71,8 @@ struct alignas(16) DevPattern {  // pattern.rs:23-27
     double color[3];
     double scale;
     int32_t kind, a, b, flags;
+    double persistence;  // Perturbed / Noise (pattern.rs:16-19)
+    int32_t octaves, pad;
 };
 
 struct alignas(16) DevLight {  // light.rs:17-21

@@ -34,18 +34,23 @@ class SceneBuilder:
         self.kind, self.parent, self.material, self.transform, self.tri, self.kids, self.top = [], [], [], [], [], [], []
         self.mats, self.mat_pattern = [], []
         self.pat_kind, self.pat_a, self.pat_b, self.pat_color, self.pat_scale, self.pat_transform = [], [], [], [], [], []
+        self.pat_octaves, self.pat_persistence = [], []
         self.light_kind, self.light, self.light_level = [], [], []
         self.shape, self.csg_op = [], []
         self._keep = None
 
     # --- materials / patterns (material.rs, pattern.rs)
-    def pattern(self, kind, color=(0.0, 0.0, 0.0), a=-1, b=-1, scale=0.5, transform=IDENTITY):
+    def pattern(self, kind, color=(0.0, 0.0, 0.0), a=-1, b=-1, scale=0.5, transform=IDENTITY, octaves=1,
+                persistence=1.0):
+        """A pattern tree node (pattern.rs:23-27); octaves / persistence are Perturbed / Noise's."""
         self.pat_kind.append(_lib.PAT[kind] if isinstance(kind, str) else int(kind))
         self.pat_a.append(a)
         self.pat_b.append(b)
         self.pat_color.extend(float(x) for x in color)
         self.pat_scale.append(float(scale))
         self.pat_transform.extend(float(x) for x in transform)
+        self.pat_octaves.append(int(octaves))
+        self.pat_persistence.append(float(persistence))
         return len(self.pat_kind) - 1
 
     def new_material(self, mat7=DEFAULT_MATERIAL, pattern=-1):
@@ -142,6 +147,8 @@ class SceneBuilder:
             "light": np.array(self.light or [0.0], np.float64),
             "light_level": np.array(self.light_level or [0], np.int32),
             "shape": np.array(self.shape or [0.0], np.float64), "csg_op": np.array(self.csg_op or [0], np.int32),
+            "pat_octaves": np.array(self.pat_octaves or [0], np.int32),
+            "pat_persistence": np.array(self.pat_persistence or [0.0], np.float64),
         }
         d = _lib.SceneDesc()
         d.n_objects = len(self.kind)

@@ -60,7 +60,9 @@ YAMLS = [(SCENES, f) for f in ("c1_readme.yaml", "c2_s1024.yaml", "c3_s1024_refl
                                "c5_area_light.yaml")] + \
         [(GOLDEN, f) for f in ("checker_pattern.yaml", "stripe_pattern.yaml", "gradient_pattern.yaml",
                                "ring_pattern.yaml", "blend_pattern.yaml", "triangle.yaml", "objects_cylinder.yaml",
-                               "objects_cone.yaml", "shapes_csg.yaml", "shapes_glass.yaml", "shapes_mixed.yaml")]
+                               "objects_cone.yaml", "shapes_csg.yaml", "shapes_glass.yaml", "shapes_mixed.yaml",
+                               "noise_pattern.yaml", "perturbed_pattern.yaml", "objects_sphere.yaml",
+                               "objects_cube.yaml", "patterns_noise_mix.yaml")]
 
 
 @pytest.mark.parametrize("root,name", YAMLS)
@@ -84,6 +86,14 @@ def test_yaml_front_end_matches_oracle_builder(R, oracle_mod, root, name):
             assert [d.shape[3 * i + k] for k in range(3)] == o.shape_params(i), (name, i)
         if d.kind[i] == 8:
             assert d.csg_op[i] == o.csg_op(i), (name, i)
+    assert d.n_patterns == o.num_patterns()
+    for j in range(d.n_patterns):  # pattern tree nodes in creation order (scene_builder_yaml.rs:226-317)
+        kind, a, b, scale, octaves, persistence = o.pattern_info(j)
+        assert (d.pat_kind[j], d.pat_a[j], d.pat_b[j]) == (kind, a, b), (name, j)
+        if kind in (6, 7, 8):
+            assert d.pat_scale[j] == scale, (name, j)
+        if kind in (7, 8):
+            assert (d.pat_octaves[j], d.pat_persistence[j]) == (octaves, persistence), (name, j)
     for f in ("hsize", "vsize", "pixel_size", "half_width", "half_height"):
         assert getattr(s.camera, f) == getattr(cam, f), f
     assert list(s.camera.transform) == list(cam.transform)
@@ -107,6 +117,12 @@ def test_yaml_edge_cases(R):
         R.YamlScene(base + "lights:\r  - type: point\r    color: [1,1,1]\r    position: [0,0,0]\r"
                     "scene:\r  - type: torus\r    minor_radius: 0.25\r", 10, 10, 1)
     assert e.value.code == -5  # RR_E_LIMIT: out-of-scope shape (next-4), reported not silently dropped
+    lights = "lights:\r  - type: point\r    color: [1,1,1]\r    position: [0,0,0]\r"
+    with pytest.raises(R.RRError) as e:
+        s = R.YamlScene(base + lights + "scene:\r  - type: sphere\r    material:\r      pattern:\r        type: noise\r"
+                    "        octaves: 1000\r        color_a: [1, 0, 0]\r        color_b: [0, 1, 0]\r", 10, 10, 1)
+        _inspect(R, s.desc())
+    assert e.value.code == -5  # octaves above RR_MAX_OCTAVES
 
 
 def test_obj_loader_counts(R):

@@ -103,10 +103,13 @@ def test_reference_example_scenes(renderer, name):
 
 @pytest.mark.parametrize("name,W,H,aa", [("shapes_csg.yaml", 64, 32, 2), ("shapes_glass.yaml", 64, 32, 2),
                                          ("shapes_mixed.yaml", 64, 32, 2), ("objects_cylinder.yaml", 48, 24, 1),
-                                         ("objects_cone.yaml", 48, 24, 1)])
+                                         ("objects_cone.yaml", 48, 24, 1), ("patterns_noise_mix.yaml", 64, 32, 2),
+                                         ("noise_pattern.yaml", 64, 32, 1), ("perturbed_pattern.yaml", 64, 32, 1),
+                                         ("objects_sphere.yaml", 48, 24, 2)])
 def test_shape_scenes(renderer, name, W, H, aa):
     """Cube / cylinder / cone / CSG through the general kernel variant: 4-entry
-    leaves, CSG subtrees evaluated per lane, n1/n2 over filtered entries."""
+    leaves, CSG subtrees evaluated per lane, n1/n2 over filtered entries.  Perturbed / noise
+    patterns (next-3): the f32 Perlin lattice restated op-for-op, nested in other patterns."""
     scene, (o, cam) = _yaml_pair(name, W, H, aa, obj_root=GOLDEN, path=os.path.join(GOLDEN, name))
     renderer.upload(scene)
     got = renderer.render(scene.camera, aa=aa, max_depth=5, canvas=True)
@@ -118,21 +121,46 @@ def test_shape_scenes(renderer, name, W, H, aa):
     assert got["stats"]["shade_events"] == st["shade_events"]
 
 
-@pytest.mark.parametrize("name,png", [("objects_cylinder.yaml", "objects_cylinder.png"),
-                                      ("objects_cone.yaml", "objects_cone.png")])
-def test_reference_png_through_gpu(renderer, R, name, png):
-    """The reference renderer's own 800x400 aa=3 outputs (examples/objects/*.png), reproduced by the
-    GPU path through quantisation (canvas.rs:76-105)."""
+@pytest.mark.parametrize("name,png,aa", [("objects_cylinder.yaml", "objects_cylinder.png", 3),
+                                         ("objects_cone.yaml", "objects_cone.png", 3),
+                                         ("objects_sphere.yaml", "objects_sphere.png", 3),
+                                         ("objects_cube.yaml", "objects_cube.png", 3),
+                                         ("noise_pattern.yaml", "noise_pattern.png", 1),
+                                         ("perturbed_pattern.yaml", "perturbed_pattern.png", 1)])
+def test_reference_png_through_gpu(renderer, R, name, png, aa):
+    """The reference renderer's own 800x400 outputs (examples/objects/*.png at aa=3,
+    examples/patterns/*.png at aa=1), reproduced by the GPU path through quantisation
+    (canvas.rs:76-105)."""
     PIL = pytest.importorskip("PIL.Image")
     text = open(os.path.join(GOLDEN, name)).read()
-    scene = R.YamlScene(text, 800, 400, 3, obj_root=GOLDEN)
+    scene = R.YamlScene(text, 800, 400, aa, obj_root=GOLDEN)
     renderer.upload(scene)
-    avg = renderer.render(scene.camera, aa=3, max_depth=5)["avg"]
+    avg = renderer.render(scene.camera, aa=aa, max_depth=5)["avg"]
     q = R.quantize(avg)[..., :3]
     ref = np.asarray(PIL.open(os.path.join(GOLDEN, "png", png)).convert("RGB"))
     diff = int((q != ref).any(axis=2).sum())
     print(f"{png}: {diff} of {ref.shape[0] * ref.shape[1]} pixels differ")
     assert diff == 0
+
+
+def test_noise_zero_octaves_is_nan(renderer, R):
+    """octave_perlin with 0 octaves returns 0/0 (noise.rs:11-29): the noise pattern's colour is NaN
+    (b * NaN), which quantises to 0 (canvas.rs `as u8`).  Both sides must agree NaN-for-NaN."""
+    from oracle.scene_yaml import build_from_yaml
+
+    text = ("camera: {fov: 60, from: [0, 1.5, -5], to: [0, 1, 0], up: [0, 1, 0]}\nlights:\n  - type: point\n"
+            "    color: [1, 1, 1]\n    position: [-10, 10, -10]\nscene:\n  - type: plane\n  - type: sphere\n"
+            "    transforms: [{type: translate, amount: [0, 1, 0]}]\n    material:\n      pattern:\n"
+            "        type: noise\n        octaves: 0\n        color_a: [1, 0, 0]\n        color_b: [0, 0, 1]\n")
+    scene = R.YamlScene(text, 32, 16, 1)
+    o, cam = build_from_yaml(text, 32, 16, 1)
+    renderer.upload(scene)
+    got = renderer.render(scene.camera, aa=1, max_depth=5)["avg"]
+    canvas, _ = o.render(cam, max_depth=5)
+    ref = o.aa_average(canvas, 1)
+    assert np.isnan(ref).any() and np.array_equal(np.isnan(got), np.isnan(ref))
+    assert np.array_equal(got, ref, equal_nan=True)
+    assert np.array_equal(R.quantize(got), o.quantize(ref))
 
 
 def test_multi_part_tiles_are_bit_identical(renderer, R):
