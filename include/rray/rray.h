@@ -46,7 +46,8 @@ enum { RR_SPHERE = 0, RR_PLANE = 1, RR_GROUP = 2, RR_TRIANGLE = 3, RR_SMOOTH_TRI
 enum { RR_CSG_UNION = 0, RR_CSG_INTERSECTION = 1, RR_CSG_DIFFERENCE = 2 };
 /* pattern kinds — PatternType (src/raytracer/material/pattern.rs:10-21), in-scope subset */
 enum { RR_PAT_TEST = 0, RR_PAT_SOLID = 1, RR_PAT_STRIPE = 2, RR_PAT_GRADIENT = 3,
-       RR_PAT_RING = 4, RR_PAT_CHECKER = 5, RR_PAT_BLEND = 6, RR_PAT_PERTURBED = 7, RR_PAT_NOISE = 8 };
+       RR_PAT_RING = 4, RR_PAT_CHECKER = 5, RR_PAT_BLEND = 6, RR_PAT_PERTURBED = 7, RR_PAT_NOISE = 8,
+       RR_PAT_TEXTURE = 9 /* pat_a = texture index */ };
 /* light kinds — LightType (src/raytracer/light.rs:10-14) */
 enum { RR_LIGHT_POINT = 0, RR_LIGHT_AREA = 1 };
 
@@ -102,6 +103,10 @@ typedef struct {
        perturbed pattern, pat_a / pat_b the noise's two sub-patterns */
     const int32_t* pat_octaves;      /* optional per pattern (`usize`, <= RR_MAX_OCTAVES); NULL: 1 */
     const double* pat_persistence;   /* optional per pattern; NULL: 1.0 */
+    /* ABI 4: image textures (texture.rs:6-11, Texture::new decodes + to_rgba8) */
+    int32_t n_textures;
+    const int32_t* tex_size;         /* n_textures x 2: width, height (>= 1 each) */
+    const uint8_t* texels;           /* RGBA8 rows top to bottom, textures back to back */
 } rr_scene_desc;
 
 /* Camera (camera.rs:18-27): hsize/vsize are the SUPERSAMPLED sizes (W*aa, H*aa). */

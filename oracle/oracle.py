@@ -65,6 +65,9 @@ def _load():
         L.orc_num_children.argtypes = [C.c_void_p, C.c_int]
         L.orc_num_objects.argtypes = [C.c_void_p]
         L.orc_num_patterns.argtypes = [C.c_void_p]
+        L.orc_add_texture.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]
+        L.orc_texture_color.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, C.POINTER(C.c_uint8)]
+        L.orc_uv_mapping.argtypes = [C.c_void_p, C.c_int, _D, _D]
         L.orc_pattern_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_double),
                                        C.POINTER(C.c_int64)]
         L.orc_get_inverse.argtypes = [C.c_void_p, C.c_int, _D]
@@ -192,7 +195,7 @@ class Mat:
 DEFAULT_MAT7 = (0.1, 0.9, 0.9, 200.0, 0.0, 0.0, 1.0)  # material.rs:47-58
 
 PAT = {"test": 0, "solid": 1, "stripe": 2, "gradient": 3, "ring": 4, "checker": 5, "blend": 6, "perturbed": 7,
-       "noise": 8}
+       "noise": 8, "texture": 9}
 KIND = {"sphere": 0, "plane": 1, "group": 2, "triangle": 3, "smooth_triangle": 4, "cube": 5, "cylinder": 6,
         "cone": 7, "csg": 8}
 CSG_OP = {"union": 0, "intersection": 1, "difference": 2}  # csg.rs:13-17
@@ -293,6 +296,22 @@ class Oracle:
 
     def num_objects(self):
         return self.L.orc_num_objects(self.w)
+
+    def add_texture(self, rgba):
+        """rgba: (height, width, 4) uint8, rows top to bottom (texture.rs:15-19)."""
+        a = np.ascontiguousarray(rgba, dtype=np.uint8)
+        assert a.ndim == 3 and a.shape[2] == 4
+        return self.L.orc_add_texture(self.w, a.shape[1], a.shape[0], a.ctypes.data_as(C.POINTER(C.c_uint8)))
+
+    def texture_color(self, tex, u, v):
+        out = (C.c_uint8 * 4)()
+        self.L.orc_texture_color(self.w, tex, float(u), float(v), out)
+        return list(out)
+
+    def uv_mapping(self, oid, p):
+        out = (C.c_double * 2)()
+        self.L.orc_uv_mapping(self.w, oid, _dv(p), out)
+        return out[0], out[1]
 
     def num_patterns(self):
         return self.L.orc_num_patterns(self.w)

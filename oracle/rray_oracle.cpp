@@ -299,8 +299,14 @@ extern "C" double orc_jitter(uint64_t seed, uint64_t sample, uint32_t path, uint
     return (double)(h >> 11) * (1.0 / 9007199254740992.0);
 }
 
+struct Texture {  // texture.rs:6-11 (RgbaImage after to_rgba8)
+    uint32_t width = 0, height = 0;
+    std::vector<uint8_t> rgba;
+};
+
 struct orc_world {
     std::vector<Object> objects;  // object/db.rs registry: index == id
+    std::vector<Texture> textures;
     std::vector<int> ids;         // Scene.ids (scene.rs:24-27)
     std::vector<Light> lights;
     std::vector<Pattern> patterns;
@@ -775,30 +781,131 @@ double octave_perlin(double x, double y, double z, int64_t octaves, double persi
     return total / max_value;
 }
 
-Color pattern_at(const orc_world* w, int pidx, const Tuple& object_point) {
+double rust_clamp(double x, double lo, double hi) {  // f64::clamp: NaN passes through
+    if (x < lo) x = lo;
+    if (x > hi) x = hi;
+    return x;
+}
+uint32_t as_u32(double f) {  // `as u32`: truncate, saturate, NaN -> 0
+    if (!(f > 0.0)) return 0;
+    if (f >= 4294967295.0) return 4294967295u;
+    return (uint32_t)f;
+}
+
+// texture.rs:31-55
+void texture_color(const Texture& t, double u, double v, uint8_t out[4]) {
+    u = rust_clamp(u, 0.0, 1.0);
+    v = rust_clamp(v, 0.0, 1.0);
+    uint32_t x = std::min(as_u32(u * (double)t.width), t.width - 1);
+    uint32_t y = std::min(as_u32(v * (double)t.height), t.height - 1);
+    y = t.height - y - 1;  // v = 0 is the bottom row
+    const uint8_t* px = &t.rgba[4 * ((size_t)y * t.width + x)];
+    for (int k = 0; k < 4; ++k) out[k] = px[k];
+}
+Color sample_texture(const Texture& t, double u, double v) {
+    uint8_t c[4];
+    texture_color(t, u, v, c);
+    return Color{(double)c[0] / 255.0, (double)c[1] / 255.0, (double)c[2] / 255.0};
+}
+
+// Object::uv_mapping: sphere.rs:126-132, plane.rs:105-113, cube.rs:132-175, cylinder.rs:181-197,
+// cone.rs:232-257, triangle.rs:148-170 (smooth_triangle.rs:151-173 is the same); groups and CSG keep
+// the trait default (0, 0) (object.rs:70-72).
+void uv_mapping(const Object& o, const Tuple& p, double& u, double& v) {
+    const double PI = 3.141592653589793;
+    switch (o.kind) {
+        case ORC_SPHERE: {
+            double theta = std::atan2(p.z, p.x);
+            double phi = std::acos(p.y / std::sqrt(p.x * p.x + p.y * p.y + p.z * p.z));
+            u = (theta + PI) / (2.0 * PI);
+            v = 1.0 - (phi / PI);
+            return;
+        }
+        case ORC_PLANE: {
+            u = std::fmod(p.x, 1.0);
+            v = std::fmod(p.z, 1.0);
+            if (u < 0.0) u = 1.0 + u;
+            if (v < 0.0) v = 1.0 + v;
+            return;
+        }
+        case ORC_CUBE: {
+            double ax = std::fabs(p.x), ay = std::fabs(p.y), az = std::fabs(p.z);
+            if (ax >= ay && ax >= az) {
+                u = p.x > 0.0 ? (p.z + 1.0) * 0.5 : (1.0 - p.z) * 0.5;
+                v = (p.y + 1.0) * 0.5;
+            } else if (ay >= ax && ay >= az) {
+                u = (p.x + 1.0) * 0.5;
+                v = p.y > 0.0 ? (1.0 - p.z) * 0.5 : (p.z + 1.0) * 0.5;
+            } else {
+                u = p.z > 0.0 ? (p.x + 1.0) * 0.5 : (1.0 - p.x) * 0.5;
+                v = (p.y + 1.0) * 0.5;
+            }
+            return;
+        }
+        case ORC_CYLINDER: {
+            if (o.closed && (p.y <= o.minimum || p.y >= o.maximum)) {
+                u = (p.x + 1.0) / 2.0;
+                v = (p.z + 1.0) / 2.0;
+                return;
+            }
+            double theta = std::atan2(p.z, p.x);
+            u = (theta + PI) / (2.0 * PI);
+            v = std::fmod(p.y, 1.0);
+            if (v < 0.0) v = 1.0 + v;
+            return;
+        }
+        case ORC_CONE: {
+            double dmin = std::fabs(p.y - o.minimum), dmax = std::fabs(p.y - o.maximum);
+            if (o.closed && (dmin <= EPSILON || dmax <= EPSILON)) {
+                double radius = std::fabs(p.y);
+                u = (p.x / radius + 1.0) / 2.0;
+                v = (p.z / radius + 1.0) / 2.0;
+                return;
+            }
+            double theta = (std::atan2(p.z, p.x) + PI) / (2.0 * PI);
+            u = (p.y - o.minimum) / (o.maximum - o.minimum);
+            v = theta;
+            return;
+        }
+        case ORC_TRIANGLE:
+        case ORC_SMOOTH_TRIANGLE: {
+            Tuple v0 = sub(o.p2, o.p1), v1 = sub(o.p3, o.p1), v2 = sub(p, o.p1);
+            double d00 = dot(v0, v0), d01 = dot(v0, v1), d11 = dot(v1, v1), d20 = dot(v2, v0), d21 = dot(v2, v1);
+            double denom = d00 * d11 - d01 * d01;
+            u = (d11 * d20 - d01 * d21) / denom;
+            v = (d00 * d21 - d01 * d20) / denom;
+            return;
+        }
+        default:
+            u = 0.0;
+            v = 0.0;
+    }
+}
+
+Color pattern_at(const orc_world* w, int pidx, const Tuple& object_point, int shape) {
     const Pattern& p = pat(w, pidx);
     Tuple pp = mul_tuple(p.inv, object_point);
     switch (p.kind) {
         case ORC_PAT_TEST: return {pp.x, pp.y, pp.z};
         case ORC_PAT_SOLID: return p.color;
         case ORC_PAT_STRIPE:
-            return (sat_i32(std::floor(pp.x)) % 2 == 0) ? pattern_at(w, p.a, pp) : pattern_at(w, p.b, pp);
+            return (sat_i32(std::floor(pp.x)) % 2 == 0) ? pattern_at(w, p.a, pp, shape) : pattern_at(w, p.b, pp, shape);
         case ORC_PAT_GRADIENT: {
-            Color a = pattern_at(w, p.a, pp);
-            Color b = pattern_at(w, p.b, pp);
+            Color a = pattern_at(w, p.a, pp, shape);
+            Color b = pattern_at(w, p.b, pp, shape);
             Color distance = csub(b, a);
             double fraction = pp.x - std::floor(pp.x);
             return cadd(a, cmul(distance, fraction));
         }
         case ORC_PAT_RING:
-            return (sat_i32(std::floor(std::sqrt(pp.x * pp.x + pp.z * pp.z))) % 2 == 0) ? pattern_at(w, p.a, pp)
-                                                                                           : pattern_at(w, p.b, pp);
+            return (sat_i32(std::floor(std::sqrt(pp.x * pp.x + pp.z * pp.z))) % 2 == 0) ? pattern_at(w, p.a, pp, shape)
+                                                                                           : pattern_at(w, p.b, pp, shape);
         case ORC_PAT_CHECKER:
-            return (sat_i32(std::floor(pp.x) + std::floor(pp.y) + std::floor(pp.z)) % 2 == 0) ? pattern_at(w, p.a, pp)
-                                                                                              : pattern_at(w, p.b, pp);
+            return (sat_i32(std::floor(pp.x) + std::floor(pp.y) + std::floor(pp.z)) % 2 == 0) ? pattern_at(w, p.a, pp, shape)
+                                                                                              : pattern_at(w, p.b, pp, shape);
         case ORC_PAT_BLEND: {
-            Color a = pattern_at(w, p.a, pp);
-            Color b = pattern_at(w, p.b, pp);
+            Color a = pattern_at(w, p.a, pp, shape);
+            Color b = pattern_at(w, p.b, pp, shape);
             return cadd(cmul(a, 1.0 - p.scale), cmul(b, p.scale));
         }
         case ORC_PAT_PERTURBED: {  // pattern.rs:187-199
@@ -806,13 +913,18 @@ Color pattern_at(const orc_world* w, int pidx, const Tuple& object_point) {
             double ny = octave_perlin(pp.x, pp.y, pp.z + 1.0, p.octaves, p.persistence) * p.scale;
             double nz = octave_perlin(pp.x, pp.y, pp.z + 2.0, p.octaves, p.persistence) * p.scale;
             Tuple np = {pp.x + nx, pp.y + ny, pp.z + nz, pp.w};
-            return pattern_at(w, p.a, np);
+            return pattern_at(w, p.a, np, shape);
         }
         case ORC_PAT_NOISE: {  // pattern.rs:200-208
             double n = octave_perlin(pp.x, pp.y, pp.z, p.octaves, p.persistence);
             n = n * p.scale;
-            if (n <= 0.0) return cmul(pattern_at(w, p.a, pp), -n);
-            return cmul(pattern_at(w, p.b, pp), n);
+            if (n <= 0.0) return cmul(pattern_at(w, p.a, pp, shape), -n);
+            return cmul(pattern_at(w, p.b, pp, shape), n);
+        }
+        case ORC_PAT_TEXTURE: {  // pattern.rs:209-213: uv of the shape being shaded
+            double u = 0.0, v = 0.0;
+            if (shape >= 0) uv_mapping(w->objects[shape], pp, u, v);
+            return sample_texture(w->textures[p.a], u, v);
         }
     }
     return BLACK;
@@ -820,7 +932,7 @@ Color pattern_at(const orc_world* w, int pidx, const Tuple& object_point) {
 // material.rs:77-80
 Color pattern_at_object(const orc_world* w, int shape, const Tuple& wp) {
     Tuple op = world_to_object(w, shape, wp);
-    return pattern_at(w, w->objects[shape].material.pattern, op);
+    return pattern_at(w, w->objects[shape].material.pattern, op, shape);
 }
 
 // light.rs:98-140
@@ -1241,7 +1353,21 @@ void orc_lighting(orc_world* w, int obj, int light, const double p[3], const dou
     out3(lighting(w, obj, w->lights[light], tp(p, 1.0), tp(e, 0.0), tp(n, 0.0), in_shadow), out);
 }
 void orc_pattern_at(orc_world* w, int pattern, const double p[3], double out[3]) {
-    out3(pattern_at(w, pattern, tp(p, 1.0)), out);
+    out3(pattern_at(w, pattern, tp(p, 1.0), -1), out);
+}
+int orc_add_texture(orc_world* w, int width, int height, const uint8_t* rgba) {
+    Texture t;
+    t.width = (uint32_t)width;
+    t.height = (uint32_t)height;
+    t.rgba.assign(rgba, rgba + 4 * (size_t)width * (size_t)height);
+    w->textures.push_back(std::move(t));
+    return (int)w->textures.size() - 1;
+}
+void orc_texture_color(orc_world* w, int tex, double u, double v, uint8_t out[4]) {
+    texture_color(w->textures[tex], u, v, out);
+}
+void orc_uv_mapping(orc_world* w, int obj, const double p[3], double out[2]) {
+    uv_mapping(w->objects[obj], tp(p, 1.0), out[0], out[1]);
 }
 void orc_normal_at(orc_world* w, int obj, const double p[3], double u, double v, double out[4]) {
     finalize(w);

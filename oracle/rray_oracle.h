@@ -29,7 +29,8 @@ typedef struct orc_world orc_world;
 
 /* pattern kinds (pattern.rs:10-21) */
 enum { ORC_PAT_TEST = 0, ORC_PAT_SOLID = 1, ORC_PAT_STRIPE = 2, ORC_PAT_GRADIENT = 3,
-       ORC_PAT_RING = 4, ORC_PAT_CHECKER = 5, ORC_PAT_BLEND = 6, ORC_PAT_PERTURBED = 7, ORC_PAT_NOISE = 8 };
+       ORC_PAT_RING = 4, ORC_PAT_CHECKER = 5, ORC_PAT_BLEND = 6, ORC_PAT_PERTURBED = 7, ORC_PAT_NOISE = 8,
+       ORC_PAT_TEXTURE = 9 /* a = texture id */ };
 /* object kinds */
 enum { ORC_SPHERE = 0, ORC_PLANE = 1, ORC_GROUP = 2, ORC_TRIANGLE = 3, ORC_SMOOTH_TRIANGLE = 4,
        ORC_CUBE = 5, ORC_CYLINDER = 6, ORC_CONE = 7, ORC_CSG = 8 };
@@ -109,6 +110,11 @@ int  orc_is_shadowed(orc_world* w, const double p[3], const double light_pos[3])
 void orc_lighting(orc_world* w, int obj, int light, const double point[3], const double eyev[3], const double normalv[3],
                   double in_shadow, double out[3]);
 void orc_pattern_at(orc_world* w, int pattern, const double p[3], double out[3]);
+/* texture.rs: RGBA8 rows top to bottom (image crate RgbaImage); returns the texture id */
+int  orc_add_texture(orc_world* w, int width, int height, const uint8_t* rgba);
+void orc_texture_color(orc_world* w, int tex, double u, double v, uint8_t out[4]);
+/* Object::uv_mapping of object `obj` at an object-space point */
+void orc_uv_mapping(orc_world* w, int obj, const double p[3], double out[2]);
 void orc_normal_at(orc_world* w, int obj, const double p[3], double u, double v, double out[4]);
 void orc_world_to_object(orc_world* w, int obj, const double p[3], double out[4]);
 void orc_normal_to_world(orc_world* w, int obj, const double n[3], double out[4]);

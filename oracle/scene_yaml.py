@@ -10,6 +10,7 @@ import math
 import os
 import re
 
+import numpy as np
 import yaml
 
 from .oracle import DEFAULT_MAT7, Mat, Oracle
@@ -128,6 +129,7 @@ class YamlSceneBuilder:
     def __init__(self, orc: Oracle, obj_root=None):
         self.o = orc
         self.obj_root = obj_root
+        self.textures = {}  # decoded image per path (each Pattern::texture holds its own copy)
 
     def color(self, v):
         return (get_f64(v[0]), get_f64(v[1]), get_f64(v[2]))
@@ -164,8 +166,17 @@ class YamlSceneBuilder:
             pid = self.o.pattern("noise", a=a, b=b, scale=scale, transform=transform)
             self.o.set_noise(pid, octaves, persistence)
             return pid
-        if ty == "image":
-            raise NotImplementedError("pattern 'image' is out of scope (SURVEY.md §8 next-3: texture)")
+        if ty == "image":  # :293-296 -> Texture::new (texture.rs:15-19): decode, to_rgba8
+            path = _get(p, "file")
+            if not isinstance(path, str):
+                raise ValueError("file not found")
+            if self.obj_root and not os.path.isabs(path):
+                path = os.path.join(self.obj_root, path)
+            if path not in self.textures:
+                from PIL import Image
+
+                self.textures[path] = self.o.add_texture(np.asarray(Image.open(path).convert("RGBA")))
+            return self.o.pattern("texture", a=self.textures[path], transform=transform)
         return self.o.pattern("solid", color=(0.0, 0.0, 0.0), transform=transform)
 
     def sub_pattern(self, transform, color, pat):  # :310-317

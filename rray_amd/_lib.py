@@ -19,7 +19,7 @@ RR_OUT_CANVAS, RR_OUT_AVG, RR_OUT_AVG_F32 = 1, 2, 4
 SPHERE, PLANE, GROUP, TRIANGLE, SMOOTH_TRIANGLE, CUBE, CYLINDER, CONE, CSG = range(9)
 CSG_OPS = {"union": 0, "intersection": 1, "difference": 2}
 PAT = {"test": 0, "solid": 1, "stripe": 2, "gradient": 3, "ring": 4, "checker": 5, "blend": 6, "perturbed": 7,
-       "noise": 8}
+       "noise": 8, "texture": 9}
 LIGHT_POINT, LIGHT_AREA = 0, 1
 KERNELS = ["trace", "n1n2", "shade", "shadow", "finish", "combine", "aa", "trace_shade"]
 
@@ -34,7 +34,8 @@ class SceneDesc(C.Structure):
                 ("n_patterns", C.c_int32), ("pat_kind", _I), ("pat_a", _I), ("pat_b", _I), ("pat_color", _D),
                 ("pat_scale", _D), ("pat_transform", _D), ("n_lights", C.c_int32), ("light_kind", _I),
                 ("light", _D), ("light_level", _I), ("shape", _D), ("csg_op", _I), ("pat_octaves", _I),
-                ("pat_persistence", _D)]
+                ("pat_persistence", _D), ("n_textures", C.c_int32), ("tex_size", _I),
+                ("texels", C.POINTER(C.c_uint8))]
 
 
 class Camera(C.Structure):

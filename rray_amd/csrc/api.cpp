@@ -64,7 +64,7 @@ struct rr_ctx {
     bool has_scene = false;
     rr::HostScene host;
     rr::DevScene S{};
-    DBuf culls, chunks, nodes, groups, shapes, tris, mats, pats, lights;
+    DBuf culls, chunks, nodes, groups, shapes, tris, mats, pats, lights, textures, texels;
     // workspace
     DBuf counters, lcount, hit, n12, n1n2, ev_a, ev_b, canvas, rays0, qout;
     std::vector<DBuf> comb, pend;  // one per level
@@ -345,7 +345,7 @@ void rr_destroy(rr_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)sync_ctx(c);
-    for (DBuf* b : {&c->culls, &c->chunks, &c->nodes, &c->groups, &c->shapes, &c->tris, &c->mats, &c->pats, &c->lights, &c->counters,
+    for (DBuf* b : {&c->culls, &c->chunks, &c->nodes, &c->groups, &c->shapes, &c->tris, &c->mats, &c->pats, &c->lights, &c->textures, &c->texels, &c->counters,
                     &c->lcount, &c->hit, &c->n12, &c->n1n2, &c->ev_a, &c->ev_b, &c->canvas, &c->rays0, &c->qout})
         b->release();
     for (auto& b : c->comb) b.release();
@@ -379,6 +379,8 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     HIPCHK(upload(c->mats, hs.mats, st));
     HIPCHK(upload(c->pats, hs.pats, st));
     HIPCHK(upload(c->lights, hs.lights, st));
+    HIPCHK(upload(c->textures, hs.textures, st));
+    HIPCHK(upload(c->texels, hs.texels, st));
     HIPCHK(hipStreamSynchronize(st));
     c->host = std::move(hs);
     rr::DevScene& S = c->S;
@@ -392,9 +394,12 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     S.mats = c->mats.as<rr::DevMaterial>();
     S.pats = c->pats.as<rr::DevPattern>();
     S.lights = c->lights.as<rr::DevLight>();
+    S.textures = c->textures.as<rr::DevTexture>();
+    S.texels = c->texels.as<uint32_t>();
     S.n_nodes = (int32_t)c->host.nodes.size();
     S.n_lights = (int32_t)c->host.lights.size();
     S.has_transparent = c->host.has_transparent;
+    S.complex_patterns = c->host.complex_patterns;
     S.has_groups = c->host.groups.empty() ? 0 : 1;
     S.general = (c->host.has_csg || c->host.has_quad) ? 1 : 0;
     const size_t lds_bytes = (size_t)S.n_nodes * sizeof(rr::DevCull) + (size_t)S.n_chunks * sizeof(rr::DevChunk);

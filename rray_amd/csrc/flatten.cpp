@@ -286,9 +286,18 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
         M4 t = d.pat_transform ? load16(d.pat_transform + 16 * (size_t)i) : identity();
         if (!inverse_3x4(t, nullptr, p.inv, nullptr, err)) return RR_E_NONAFFINE;
         p.flags = is_identity12(p.inv) ? NF_IDENT : 0;
-        if (p.kind < RR_PAT_TEST || p.kind > RR_PAT_NOISE) {
+        if (p.kind < RR_PAT_TEST || p.kind > RR_PAT_TEXTURE) {
             err = "unknown pattern kind";
             return RR_E_ARG;
+        }
+        if (p.kind == RR_PAT_TEXTURE) {
+            if (p.a < 0 || p.a >= d.n_textures) {
+                err = "texture pattern references an unknown texture";
+                return RR_E_ARG;
+            }
+            out.complex_patterns = 1;
+            out.pats.push_back(p);
+            continue;
         }
         if ((p.kind == RR_PAT_PERTURBED || p.kind == RR_PAT_NOISE) && (p.octaves < 0 || p.octaves > RR_MAX_OCTAVES)) {
             err = "pattern octaves outside [0, RR_MAX_OCTAVES]";
@@ -300,13 +309,14 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
             err = "pattern child index out of range";
             return RR_E_ARG;
         }
+        if (p.kind == RR_PAT_GRADIENT || p.kind == RR_PAT_BLEND || p.kind >= RR_PAT_PERTURBED) out.complex_patterns = 1;
         out.pats.push_back(p);
     }
     // pattern nesting depth (the kernel evaluates trees with a bounded explicit stack)
     std::function<int(int, int)> pdepth = [&](int i, int lvl) -> int {
         if (lvl > RR_MAX_PATTERN_DEPTH) return lvl;
         const DevPattern& p = out.pats[i];
-        if (p.kind == RR_PAT_TEST || p.kind == RR_PAT_SOLID) return lvl;
+        if (p.kind == RR_PAT_TEST || p.kind == RR_PAT_SOLID || p.kind == RR_PAT_TEXTURE) return lvl;
         if (p.kind == RR_PAT_PERTURBED) return pdepth(p.a, lvl + 1);
         return std::max(pdepth(p.a, lvl + 1), pdepth(p.b, lvl + 1));
     };
@@ -315,6 +325,27 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
             err = "pattern nesting exceeds RR_MAX_PATTERN_DEPTH";
             return RR_E_LIMIT;
         }
+    // textures
+    if (d.n_textures < 0 || (d.n_textures > 0 && (!d.tex_size || !d.texels))) {
+        err = "texture arrays missing";
+        return RR_E_ARG;
+    }
+    for (int i = 0; i < d.n_textures; ++i) {
+        int32_t w = d.tex_size[2 * i], h = d.tex_size[2 * i + 1];
+        if (w < 1 || h < 1) {
+            err = "texture with an empty image";
+            return RR_E_ARG;
+        }
+        DevTexture t{};
+        t.offset = out.texels.size();
+        t.width = (uint32_t)w;
+        t.height = (uint32_t)h;
+        const uint8_t* px = d.texels + 4 * t.offset;
+        for (size_t k = 0; k < (size_t)w * (size_t)h; ++k)
+            out.texels.push_back((uint32_t)px[4 * k] | ((uint32_t)px[4 * k + 1] << 8) | ((uint32_t)px[4 * k + 2] << 16) |
+                                 ((uint32_t)px[4 * k + 3] << 24));
+        out.textures.push_back(t);
+    }
     // lights
     for (int i = 0; i < d.n_lights; ++i) {
         DevLight l{};

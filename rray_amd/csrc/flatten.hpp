@@ -18,11 +18,14 @@ struct HostScene {
     std::vector<DevMaterial> mats;
     std::vector<DevPattern> pats;
     std::vector<DevLight> lights;
+    std::vector<DevTexture> textures;
+    std::vector<uint32_t> texels;
     std::vector<int32_t> node_of_object;  // object id -> node index (-1 if not in the scene tree)
     int32_t has_transparent = 0;
-    int32_t has_secondary = 0;
+    int32_t has_secondary = 0;            // some material reflective != 0 or transparency != 0
     int32_t has_csg = 0;
-    int32_t has_quad = 0;                 // cubes, cylinders, cones (general kernel variant)            // some material reflective != 0 or transparency != 0
+    int32_t has_quad = 0;
+    int32_t complex_patterns = 0;         // tree-evaluated patterns (pattern_tree)                 // cubes, cylinders, cones (general kernel variant)
     int64_t n_top_leaves = 0;             // leaves tested by every ray (reference full scan)
 };
 

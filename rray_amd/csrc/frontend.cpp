@@ -31,6 +31,9 @@ struct rr_scene {
     std::vector<double> pat_color, pat_scale, pat_transform;
     std::vector<int32_t> pat_octaves;
     std::vector<double> pat_persistence;
+    std::vector<int32_t> tex_size;  // width, height per texture
+    std::vector<uint8_t> texels;    // RGBA8, textures back to back
+    std::vector<std::pair<std::string, int>> tex_of_path;  // one decode per file
     std::vector<int32_t> light_kind, light_level;
     std::vector<double> light;
     std::vector<double> shape;      // minimum, maximum, closed per object (cylinder / cone)
@@ -77,6 +80,9 @@ struct rr_scene {
         desc.csg_op = csg_op.data();
         desc.pat_octaves = pat_octaves.data();
         desc.pat_persistence = pat_persistence.data();
+        desc.n_textures = (int32_t)(tex_size.size() / 2);
+        desc.tex_size = tex_size.data();
+        desc.texels = texels.data();
     }
 };
 
@@ -193,14 +199,35 @@ struct Builder {
             int b = sub_pattern(transform, p["color_b"], p["pattern_b"]);
             return add_pattern(RR_PAT_NOISE, transform, 0, 0, 0, a, b, scale, octaves, persistence);
         }
-        if (ty.s == "image")
-            panic("pattern 'image' is outside the GPU path's scope (SURVEY.md §8 next-3: texture)", RR_E_LIMIT);
+        if (ty.s == "image") {  // :293-296 -> Texture::new (texture.rs:15-19)
+            const Node& file = p["file"];
+            if (file.kind != Node::String) panic("file not found");
+            return add_pattern(RR_PAT_TEXTURE, transform, 0, 0, 0, load_texture(file.s));
+        }
         return add_pattern(RR_PAT_SOLID, transform, 0, 0, 0);
     }
     // `f64 as usize` (saturating, NaN -> 0); counts above RR_MAX_OCTAVES are rejected at upload
     static int32_t as_octaves(double v) {
         if (!(v > 0)) return 0;
         return v >= 2147483647.0 ? 2147483647 : (int32_t)v;
+    }
+    int load_texture(const std::string& file) {
+        std::string path = file;
+        if (!obj_root.empty() && !file.empty() && file[0] != '/') path = obj_root + "/" + file;
+        for (auto& e : S.tex_of_path)
+            if (e.first == path) return e.second;
+        std::vector<uint8_t> rgba;
+        uint32_t w = 0, h = 0;
+        std::string err;
+        int rc = rr::read_png_rgba(path, rgba, w, h, err);
+        if (rc != RR_OK) panic(err, rc);
+        if (w > 0x7fffffffu || h > 0x7fffffffu) panic(path + ": texture too large", RR_E_LIMIT);
+        int id = (int)(S.tex_size.size() / 2);
+        S.tex_size.push_back((int32_t)w);
+        S.tex_size.push_back((int32_t)h);
+        S.texels.insert(S.texels.end(), rgba.begin(), rgba.end());
+        S.tex_of_path.emplace_back(path, id);
+        return id;
     }
     int sub_pattern(const rr::M4& t, const Node& color, const Node& pat) {  // :310-317
         if (color.is_array()) {

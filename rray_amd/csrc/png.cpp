@@ -4,8 +4,13 @@
 
 #include <zlib.h>
 
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <vector>
+
+#include "../../include/rray/rray.h"
 
 namespace rr {
 namespace {
@@ -23,7 +28,140 @@ void chunk(std::vector<uint8_t>& out, const char* type, const std::vector<uint8_
     uLong crc = crc32(0L, out.data() + start, (uInt)(out.size() - start));
     put32(out, (uint32_t)crc);
 }
+uint32_t get32(const uint8_t* p) { return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]; }
+int paeth(int a, int b, int c) {
+    int p = a + b - c, pa = std::abs(p - a), pb = std::abs(p - b), pc = std::abs(p - c);
+    if (pa <= pb && pa <= pc) return a;
+    return pb <= pc ? b : c;
+}
 }  // namespace
+
+int read_png_rgba(const std::string& path, std::vector<uint8_t>& rgba, uint32_t& width, uint32_t& height,
+                  std::string& err) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) {
+        err = "cannot open texture " + path;
+        return RR_E_IO;
+    }
+    std::vector<uint8_t> file;
+    uint8_t buf[65536];
+    size_t n;
+    while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) file.insert(file.end(), buf, buf + n);
+    std::fclose(f);
+    static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+    if (file.size() < 8 || std::memcmp(file.data(), sig, 8) != 0) {
+        err = path + ": not a PNG file (other image formats need a host-side decoder: pass texels in rr_scene_desc)";
+        return RR_E_LIMIT;
+    }
+    uint32_t w = 0, h = 0;
+    int depth = 0, ctype = -1, interlace = 0;
+    std::vector<uint8_t> idat, plte;
+    size_t pos = 8;
+    bool end = false;
+    while (!end && pos + 12 <= file.size()) {
+        uint32_t len = get32(&file[pos]);
+        if (pos + 12 + (size_t)len > file.size()) break;
+        const uint8_t* type = &file[pos + 4];
+        const uint8_t* data = &file[pos + 8];
+        if (!std::memcmp(type, "IHDR", 4) && len >= 13) {
+            w = get32(data);
+            h = get32(data + 4);
+            depth = data[8];
+            ctype = data[9];
+            interlace = data[12];
+        } else if (!std::memcmp(type, "PLTE", 4)) {
+            plte.assign(data, data + len);
+        } else if (!std::memcmp(type, "IDAT", 4)) {
+            idat.insert(idat.end(), data, data + len);
+        } else if (!std::memcmp(type, "IEND", 4)) {
+            end = true;
+        }
+        pos += 12 + (size_t)len;
+    }
+    if (w == 0 || h == 0 || ctype < 0 || idat.empty()) {
+        err = path + ": corrupt PNG";
+        return RR_E_IO;
+    }
+    const int channels = ctype == 0 ? 1 : ctype == 2 ? 3 : ctype == 3 ? 1 : ctype == 4 ? 2 : ctype == 6 ? 4 : 0;
+    const bool sub8 = depth < 8 && (ctype == 0 || ctype == 3);
+    if (channels == 0 || interlace != 0 || !(depth == 8 || (sub8 && (depth == 1 || depth == 2 || depth == 4)))) {
+        err = path + ": PNG layout outside the texture decoder (16-bit or interlaced)";
+        return RR_E_LIMIT;
+    }
+    if (ctype == 3 && plte.size() < 3) {
+        err = path + ": palette PNG without PLTE";
+        return RR_E_IO;
+    }
+    const size_t stride = ((size_t)w * channels * depth + 7) / 8;
+    const size_t bpp = std::max<size_t>(1, (size_t)channels * depth / 8);
+    std::vector<uint8_t> raw((stride + 1) * h);
+    z_stream zs{};
+    if (inflateInit(&zs) != Z_OK) {
+        err = "zlib init failed";
+        return RR_E_IO;
+    }
+    zs.next_in = idat.data();
+    zs.avail_in = (uInt)idat.size();
+    zs.next_out = raw.data();
+    zs.avail_out = (uInt)raw.size();
+    int zr = inflate(&zs, Z_FINISH);
+    inflateEnd(&zs);
+    if ((zr != Z_STREAM_END && zr != Z_BUF_ERROR) || zs.avail_out != 0) {
+        err = path + ": corrupt PNG image data";
+        return RR_E_IO;
+    }
+    // unfilter in place (filter types 0-4)
+    std::vector<uint8_t> prev(stride, 0);
+    for (uint32_t y = 0; y < h; ++y) {
+        uint8_t* row = &raw[(size_t)y * (stride + 1)];
+        uint8_t ft = row[0];
+        uint8_t* cur = row + 1;
+        for (size_t i = 0; i < stride; ++i) {
+            int a = i >= bpp ? cur[i - bpp] : 0, b = prev[i], c = i >= bpp ? prev[i - bpp] : 0;
+            int pred = ft == 0 ? 0 : ft == 1 ? a : ft == 2 ? b : ft == 3 ? (a + b) / 2 : ft == 4 ? paeth(a, b, c) : -1;
+            if (pred < 0) {
+                err = path + ": bad PNG filter type";
+                return RR_E_IO;
+            }
+            cur[i] = (uint8_t)(cur[i] + pred);
+        }
+        std::memcpy(prev.data(), cur, stride);
+    }
+    rgba.assign((size_t)w * h * 4, 255);
+    for (uint32_t y = 0; y < h; ++y) {
+        const uint8_t* cur = &raw[(size_t)y * (stride + 1) + 1];
+        for (uint32_t x = 0; x < w; ++x) {
+            uint8_t* o = &rgba[4 * ((size_t)y * w + x)];
+            if (sub8 || ctype == 3) {
+                size_t bit = (size_t)x * depth;
+                int v = (cur[bit / 8] >> (8 - depth - (int)(bit % 8))) & ((1 << depth) - 1);
+                if (ctype == 3) {
+                    if (3 * (size_t)v + 2 >= plte.size()) {
+                        err = path + ": palette index out of range";
+                        return RR_E_IO;
+                    }
+                    o[0] = plte[3 * v];
+                    o[1] = plte[3 * v + 1];
+                    o[2] = plte[3 * v + 2];
+                } else {  // grey scaled to 8 bits
+                    uint8_t g = (uint8_t)(v * 255 / ((1 << depth) - 1));
+                    o[0] = o[1] = o[2] = g;
+                }
+                continue;
+            }
+            const uint8_t* p = cur + (size_t)x * channels;
+            switch (ctype) {
+                case 0: o[0] = o[1] = o[2] = p[0]; break;
+                case 4: o[0] = o[1] = o[2] = p[0]; o[3] = p[1]; break;
+                case 2: o[0] = p[0]; o[1] = p[1]; o[2] = p[2]; break;
+                default: o[0] = p[0]; o[1] = p[1]; o[2] = p[2]; o[3] = p[3]; break;
+            }
+        }
+    }
+    width = w;
+    height = h;
+    return RR_OK;
+}
 
 bool write_png_rgba(const char* path, const uint8_t* rgba, uint32_t w, uint32_t h) {
     std::vector<uint8_t> raw;

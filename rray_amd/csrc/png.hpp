@@ -1,7 +1,15 @@
-// png.hpp — RGBA8 PNG writer (canvas.rs:124-131 writes RGBA8 through the image crate).
+// png.hpp — RGBA8 PNG writer (canvas.rs:124-131 writes RGBA8 through the image crate) and the
+// texture reader (texture.rs:15-19: decode, to_rgba8).
 #pragma once
 #include <cstdint>
+#include <string>
+#include <vector>
 
 namespace rr {
 bool write_png_rgba(const char* path, const uint8_t* rgba, uint32_t width, uint32_t height);
+// 8-bit grey / grey+alpha / RGB / RGBA and 1-8 bit palette or grey, non-interlaced; rows top to
+// bottom as RGBA8.  Returns RR_OK, RR_E_IO (unreadable / corrupt) or RR_E_LIMIT (16-bit or
+// interlaced: outside this decoder).
+int read_png_rgba(const std::string& path, std::vector<uint8_t>& rgba, uint32_t& width, uint32_t& height,
+                  std::string& err);
 }

@@ -353,13 +353,19 @@ __device__ __forceinline__ void light_step(const DevScene& S, const LevelArgs& A
 // are parked and lighting runs after each walk.
 // The prelit variant is held to 4 waves/SIMD (<= 128 VGPRs; ~10 VGPRs spill, measured faster than
 // 3 spill-free waves: C2 0.258 vs 0.288 ms/frame).  RR_SHADE_W3 builds the spill-free variant.
+// The general variant (G = 2) is not held to 4 waves: squeezed into 128 VGPRs it spills ~300
+// registers, and those builds (ROCm 7.2 clang) returned wrong, run-to-run different images for
+// cube / cylinder / CSG scenes with secondary rays, while every spill-free build is bit-exact.
 #ifndef RR_SHADE_W3
-#define RR_SHADE_ATTR(PRE) __attribute__((amdgpu_waves_per_eu((PRE) ? 4 : 2)))
+#define RR_SHADE_ATTR(PRE, G) __attribute__((amdgpu_waves_per_eu(((PRE) && (G) < 2) ? 4 : 2)))
 #else
-#define RR_SHADE_ATTR(PRE)
+#define RR_SHADE_ATTR(PRE, G)
 #endif
-template <int G, bool LC, bool FUSED, bool PRE>
-__global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE) shade_kernel(DevScene S, LevelArgs A) {
+// CP: the scene has Gradient / Blend / Perturbed / Noise / Texture patterns, evaluated by the
+// out-of-line pattern_tree.  Without CP the kernel carries no call at all: the call graph's register
+// demand (atan2 / acos / Perlin in the callee) otherwise costs the common scenes their occupancy.
+template <int G, bool LC, bool FUSED, bool PRE, bool CP>
+__global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevScene S, LevelArgs A) {
     if (LC) stage_culls(S);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < A.n;
@@ -424,7 +430,7 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE) shade_kernel(DevScene 
             c.n1 = A.n12[2 * i];
             c.n2 = A.n12[2 * i + 1];
         }
-        pcol = pattern_at(S, m.pattern, world_to_object(S, hr.node, c.over));  // material.rs:77-80
+        pcol = pattern_at<CP>(S, m.pattern, world_to_object(S, hr.node, c.over), hr.node);  // material.rs:77-80
         if (PRE) {
             double* pl = prelit_lds(S, LC);
             for (int li = 0; li < S.n_lights; ++li) {
@@ -637,16 +643,29 @@ struct Span {  // brackets one launch with events when profiling
 };
 }  // namespace
 
+template <int G, bool LC, bool FUSED>
+static void launch_shade(const DevScene& S, const LevelArgs& A, hipStream_t st, bool pre, size_t lds) {
+    const dim3 grid(blocks_for(A.n)), block(256);
+    if (S.complex_patterns) {
+        if (pre)
+            hipLaunchKernelGGL((shade_kernel<G, LC, FUSED, true, true>), grid, block, lds, st, S, A);
+        else
+            hipLaunchKernelGGL((shade_kernel<G, LC, FUSED, false, true>), grid, block, lds, st, S, A);
+    } else {
+        if (pre)
+            hipLaunchKernelGGL((shade_kernel<G, LC, FUSED, true, false>), grid, block, lds, st, S, A);
+        else
+            hipLaunchKernelGGL((shade_kernel<G, LC, FUSED, false, false>), grid, block, lds, st, S, A);
+    }
+}
+
 template <int G, bool LC>
 static void launch_level_t(const DevScene& S, const LevelArgs& A, hipStream_t st, KernelProf* prof) {
     const bool pre = S.n_lights <= RR_PRELIT_LIGHTS;
     const size_t shade_lds = cull_lds(S) + (pre ? (size_t)S.n_lights * 6 * 256 * sizeof(double) : 0);
     if (!S.has_transparent && !std::getenv("RRAY_UNFUSED")) {  // trace + shade in one kernel
         Span s(prof, K_TRACE_SHADE, st);
-        if (pre)
-            hipLaunchKernelGGL((shade_kernel<G, LC, true, true>), dim3(blocks_for(A.n)), dim3(256), shade_lds, st, S, A);
-        else
-            hipLaunchKernelGGL((shade_kernel<G, LC, true, false>), dim3(blocks_for(A.n)), dim3(256), shade_lds, st, S, A);
+        launch_shade<G, LC, true>(S, A, st, pre, shade_lds);
         return;
     }
     {
@@ -659,10 +678,7 @@ static void launch_level_t(const DevScene& S, const LevelArgs& A, hipStream_t st
     }
     {
         Span s(prof, K_SHADE, st);
-        if (pre)
-            hipLaunchKernelGGL((shade_kernel<G, LC, false, true>), dim3(blocks_for(A.n)), dim3(256), shade_lds, st, S, A);
-        else
-            hipLaunchKernelGGL((shade_kernel<G, LC, false, false>), dim3(blocks_for(A.n)), dim3(256), shade_lds, st, S, A);
+        launch_shade<G, LC, false>(S, A, st, pre, shade_lds);
     }
 }
 

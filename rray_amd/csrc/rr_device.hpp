@@ -82,6 +82,13 @@ struct alignas(16) DevLight {  // light.rs:17-21
     int32_t kind, level;
 };
 
+// Image texture (texture.rs:6-11): RGBA8 texels packed one u32 each (byte 0 = red), rows top to
+// bottom, at texels[offset ..].
+struct alignas(16) DevTexture {
+    uint64_t offset;
+    uint32_t width, height;
+};
+
 struct DevCamera {
     int64_t hsize, vsize;
     double half_width, half_height, pixel_size;
@@ -114,6 +121,8 @@ struct DevScene {
     const DevPattern* pats;
     const DevLight* lights;
     const DevShape* shapes;
+    const DevTexture* textures;
+    const uint32_t* texels;
     int32_t n_nodes, n_lights;
     int32_t n_chunks;
     int32_t pad2;
@@ -121,6 +130,8 @@ struct DevScene {
     int32_t has_groups;
     int32_t general;          // CSGs or cylinders / cones present: the kernels' G = 2 variant
     int32_t lds_culls;        // culls + chunks staged in LDS per workgroup (fits in RR_LDS_CULL_BYTES)
+    int32_t complex_patterns; // some pattern is Gradient / Blend / Perturbed / Noise / Texture
+    int32_t pad3;
 };
 // Node culls (16 B each) and chunk records (32 B each) are copied into LDS by every walking
 // workgroup when together they fit in this many bytes.

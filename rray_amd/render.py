@@ -35,6 +35,7 @@ class SceneBuilder:
         self.mats, self.mat_pattern = [], []
         self.pat_kind, self.pat_a, self.pat_b, self.pat_color, self.pat_scale, self.pat_transform = [], [], [], [], [], []
         self.pat_octaves, self.pat_persistence = [], []
+        self.textures = []  # (height, width, 4) uint8 RGBA arrays
         self.light_kind, self.light, self.light_level = [], [], []
         self.shape, self.csg_op = [], []
         self._keep = None
@@ -52,6 +53,15 @@ class SceneBuilder:
         self.pat_octaves.append(int(octaves))
         self.pat_persistence.append(float(persistence))
         return len(self.pat_kind) - 1
+
+    def texture(self, rgba):
+        """Register an RGBA8 image (rows top to bottom, texture.rs:15-19); returns its index for
+        pattern("texture", a=index)."""
+        a = np.ascontiguousarray(rgba, dtype=np.uint8)
+        if a.ndim != 3 or a.shape[2] != 4 or a.shape[0] < 1 or a.shape[1] < 1:
+            raise ValueError("texture must be a non-empty (height, width, 4) uint8 array")
+        self.textures.append(a)
+        return len(self.textures) - 1
 
     def new_material(self, mat7=DEFAULT_MATERIAL, pattern=-1):
         self.mats.extend(float(x) for x in mat7)
@@ -150,14 +160,22 @@ class SceneBuilder:
             "pat_octaves": np.array(self.pat_octaves or [0], np.int32),
             "pat_persistence": np.array(self.pat_persistence or [0.0], np.float64),
         }
+        tex_size = [v for t in self.textures for v in (t.shape[1], t.shape[0])]
+        texels = np.concatenate([t.reshape(-1) for t in self.textures]) if self.textures else np.zeros(4, np.uint8)
+        arr["tex_size"] = np.array(tex_size or [0], np.int32)
+        arr["texels"] = texels
         d = _lib.SceneDesc()
         d.n_objects = len(self.kind)
         d.n_top = len(self.top)
         d.n_materials = len(self.mat_pattern)
         d.n_patterns = len(self.pat_kind)
         d.n_lights = len(self.light_kind)
+        d.n_textures = len(self.textures)
         for k, v in arr.items():
-            setattr(d, k, _dp(v) if v.dtype == np.float64 else _ip(v))
+            if v.dtype == np.uint8:
+                setattr(d, k, v.ctypes.data_as(C.POINTER(C.c_uint8)))
+            else:
+                setattr(d, k, _dp(v) if v.dtype == np.float64 else _ip(v))
         d.inverse = None
         self._keep = arr
         return d

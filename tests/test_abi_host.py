@@ -62,7 +62,7 @@ YAMLS = [(SCENES, f) for f in ("c1_readme.yaml", "c2_s1024.yaml", "c3_s1024_refl
                                "ring_pattern.yaml", "blend_pattern.yaml", "triangle.yaml", "objects_cylinder.yaml",
                                "objects_cone.yaml", "shapes_csg.yaml", "shapes_glass.yaml", "shapes_mixed.yaml",
                                "noise_pattern.yaml", "perturbed_pattern.yaml", "objects_sphere.yaml",
-                               "objects_cube.yaml", "patterns_noise_mix.yaml")]
+                               "objects_cube.yaml", "patterns_noise_mix.yaml", "textures_mix.yaml")]
 
 
 @pytest.mark.parametrize("root,name", YAMLS)
@@ -191,3 +191,31 @@ def test_shape_and_csg_descriptor_checks(R):
     with pytest.raises(R.RRError) as e:
         _inspect(R, b.desc())
     assert e.value.code == R._lib.RR_E_LIMIT
+
+
+def test_png_texture_decoder_matches_pil(R):
+    """The product front-end's PNG reader (texture.rs:15-19: decode, to_rgba8) against PIL on RGB,
+    4-bit palette, grey and RGBA files: the colour channels the sampler reads must be identical."""
+    from PIL import Image
+
+    files = ["tex_grid.png", "tex_pal.png", "tex_grey.png", "test_texture.png", "triangle.png"]
+    scene = "".join(f"  - type: sphere\n    material: {{pattern: {{type: image, file: 'png/{f}'}}}}\n" for f in files)
+    text = ("camera: {fov: 60, from: [0, 0, -5], to: [0, 0, 0], up: [0, 1, 0]}\nlights:\n  - type: point\n"
+            "    color: [1, 1, 1]\n    position: [0, 0, -5]\nscene:\n" + scene)
+    s = R.YamlScene(text, 8, 8, 1, obj_root=GOLDEN)
+    d = s.desc()
+    assert d.n_textures == len(files)
+    off = 0
+    for i, f in enumerate(files):
+        w, h = d.tex_size[2 * i], d.tex_size[2 * i + 1]
+        got = np.ctypeslib.as_array(d.texels, shape=(off + w * h * 4,))[off:].reshape(h, w, 4)
+        ref = np.asarray(Image.open(os.path.join(GOLDEN, "png", f)).convert("RGBA"))
+        assert got.shape == ref.shape, f
+        assert np.array_equal(got[..., :3], ref[..., :3]), f
+        off += w * h * 4
+    # the same file twice is decoded once (both patterns share the texture)
+    s2 = R.YamlScene(text.replace("tex_pal", "tex_grid"), 8, 8, 1, obj_root=GOLDEN)
+    assert s2.desc().n_textures == len(files) - 1
+    with pytest.raises(R.RRError) as e:
+        R.YamlScene(text.replace("tex_grid.png", "missing.png"), 8, 8, 1, obj_root=GOLDEN)
+    assert e.value.code == R._lib.RR_E_IO

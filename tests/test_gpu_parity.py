@@ -105,11 +105,13 @@ def test_reference_example_scenes(renderer, name):
                                          ("shapes_mixed.yaml", 64, 32, 2), ("objects_cylinder.yaml", 48, 24, 1),
                                          ("objects_cone.yaml", 48, 24, 1), ("patterns_noise_mix.yaml", 64, 32, 2),
                                          ("noise_pattern.yaml", 64, 32, 1), ("perturbed_pattern.yaml", 64, 32, 1),
-                                         ("objects_sphere.yaml", 48, 24, 2)])
+                                         ("objects_sphere.yaml", 48, 24, 2), ("textures_mix.yaml", 96, 48, 2),
+                                         ("textures_mix.yaml", 200, 100, 1)])
 def test_shape_scenes(renderer, name, W, H, aa):
     """Cube / cylinder / cone / CSG through the general kernel variant: 4-entry
     leaves, CSG subtrees evaluated per lane, n1/n2 over filtered entries.  Perturbed / noise
-    patterns (next-3): the f32 Perlin lattice restated op-for-op, nested in other patterns."""
+    patterns (next-3): the f32 Perlin lattice restated op-for-op, nested in other patterns.  Image
+    textures (next-3): uv_mapping per shape kind + texel fetch from the decoded PNGs."""
     scene, (o, cam) = _yaml_pair(name, W, H, aa, obj_root=GOLDEN, path=os.path.join(GOLDEN, name))
     renderer.upload(scene)
     got = renderer.render(scene.camera, aa=aa, max_depth=5, canvas=True)

@@ -6,8 +6,12 @@ reference quotes a value to full f64 precision we additionally require the oracl
 reproduce it EXACTLY, which pins the op order (no FMA, left-to-right sums, w-inclusive dots).
 """
 import math
+import os
 
+import numpy as np
 import pytest
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 S2 = math.sqrt(2.0)
 EPS = 1e-5
@@ -434,3 +438,57 @@ def test_filtering_a_list_of_intersections(oracle_mod):  # csg.rs: filtering_a_l
         s2 = o.add("sphere", c)
         xs = [(1.0, s1), (2.0, s2), (3.0, s1), (4.0, s2)]
         assert o.csg_filter(c, xs) == keep
+
+
+def test_texture_get_color(oracle_mod):  # texture.rs:61-82 (examples/test_texture.png, 5x5 RGBA)
+    from PIL import Image
+
+    o = oracle_mod.Oracle()
+    img = np.asarray(Image.open(os.path.join(GOLDEN, "png", "test_texture.png")).convert("RGBA"))
+    t = o.add_texture(img)
+    black, blue = [0, 0, 0, 255], [19, 73, 151, 255]
+    E = 0.00001  # crate::EPSILON
+    cases = [((0.0, 0.0), black), ((1.0, 1.0), black), ((0.0, 1.0), blue), ((1.0, 0.0), blue), ((0.5, 0.5), blue),
+             ((0.2, 0.8 - E), blue), ((0.4, 0.6 - E), blue), ((0.6, 0.4 - E), blue), ((0.8, 0.2 - E), blue)]
+    for (u, v), want in cases:
+        assert o.texture_color(t, u, v) == want, (u, v)
+    # clamp keeps NaN (f64::clamp) and `as u32` maps it to 0: column 0, flipped row h-1
+    assert o.texture_color(t, math.nan, math.nan) == list(img[4, 0])
+
+
+def test_uv_mapping_properties(oracle_mod):
+    """Object::uv_mapping (sphere.rs:126-132, plane.rs:105-113, cube.rs:132-175, cylinder.rs:181-197,
+    cone.rs:232-257, triangle.rs:148-170).  The reference has no uv tests: these are properties of
+    the formulas (parity unpinned beyond them)."""
+    o = oracle_mod.Oracle()
+    s = o.add("sphere")
+    p = o.add("plane")
+    c = o.add("cube")
+    cy = o.add("cylinder")
+    o.set_shape_params(cy, 0.0, 2.0, True)
+    tri = o.add_triangle((0, 0, 0), (1, 0, 0), (0, 1, 0))
+    assert o.uv_mapping(s, (0, 1, 0)) == (0.5, 1.0)           # north pole: phi 0
+    assert o.uv_mapping(s, (-1, 0, 0)) == (1.0, 0.5)          # atan2(0, -1) = pi
+    assert o.uv_mapping(p, (-0.25, 0, 3.5)) == (0.75, 0.5)    # fmod wrapped into [0, 1)
+    assert o.uv_mapping(c, (1, 0.5, -0.5)) == (0.25, 0.75)    # right face
+    assert o.uv_mapping(c, (0.5, -1, 0.5)) == (0.75, 0.75)    # bottom face
+    assert o.uv_mapping(cy, (0.5, 2.0, -0.5)) == (0.75, 0.25)  # closed cap
+    assert o.uv_mapping(cy, (1, 1.75, 0)) == (0.5, 0.75)      # side: v = y % 1
+    assert o.uv_mapping(cy, (1, -0.25, 0)) == (1.0, 0.5)      # closed, y <= minimum: cap formula
+    assert o.uv_mapping(tri, (0.25, 0.5, 0)) == (0.25, 0.5)   # barycentric (lambda1, lambda2)
+    g = o.add("group")
+    assert o.uv_mapping(g, (3, 4, 5)) == (0.0, 0.0)           # trait default (object.rs:70-72)
+
+
+def test_perlin_properties(oracle_mod):
+    """fastnoise-lite Perlin: zero on the lattice, bounded by 1 after its 0.9649 scale; octave_perlin
+    with 0 octaves is 0/0 (noise.rs:50-63).  The values themselves are pinned by the reference PNGs
+    (tests/test_oracle_png.py: noise_pattern, perturbed_pattern, objects/sphere, objects/cube)."""
+    lib = oracle_mod.Oracle().L
+    assert lib.orc_noise_3d(0.0, 0.0, 0.0) == 0.0
+    rng = np.random.default_rng(7)
+    v = np.array([lib.orc_noise_3d(*(rng.uniform(-1000, 1000, 3))) for _ in range(2000)])
+    assert np.all(np.abs(v) <= 1.0) and v.std() > 0.1
+    assert math.isnan(lib.orc_octave_perlin(1.0, 2.0, 3.0, 0, 0.5))
+    x = lib.orc_octave_perlin(10.0, 20.0, 30.0, 1, 0.5)
+    assert x == lib.orc_noise_3d(10.0, 20.0, 30.0)
