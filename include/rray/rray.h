@@ -38,10 +38,10 @@ extern "C" {
 #define RR_E_IO (-6)         /* file missing / unreadable / unwritable */
 #define RR_E_NAN (-7)        /* NaN intersection t: reference panics in sort (scene.rs:104) */
 
-/* object kinds — Sphere, Plane, Group, Triangle, SmoothTriangle, Cube, Cylinder, Cone, Csg
+/* object kinds — Sphere, Plane, Group, Triangle, SmoothTriangle, Cube, Cylinder, Cone, Csg, Torus
  * (src/raytracer/object/) */
 enum { RR_SPHERE = 0, RR_PLANE = 1, RR_GROUP = 2, RR_TRIANGLE = 3, RR_SMOOTH_TRIANGLE = 4,
-       RR_CUBE = 5, RR_CYLINDER = 6, RR_CONE = 7, RR_CSG = 8 };
+       RR_CUBE = 5, RR_CYLINDER = 6, RR_CONE = 7, RR_CSG = 8, RR_TORUS = 9 };
 /* CSG operations — CsgOperation (csg.rs:13-17) */
 enum { RR_CSG_UNION = 0, RR_CSG_INTERSECTION = 1, RR_CSG_DIFFERENCE = 2 };
 /* pattern kinds — PatternType (src/raytracer/material/pattern.rs:10-21), in-scope subset */
@@ -96,7 +96,8 @@ typedef struct {
 
     /* ABI 3 */
     const double* shape;         /* optional n_objects x 3: minimum, maximum, closed (cylinder.rs:29-37,
-                                    cone.rs:30-38); NULL: -inf, +inf, open */
+                                    cone.rs:30-38); NULL: -inf, +inf, open.  Torus (ABI 4):
+                                    shape[0] = minor_radius (torus.rs:23-31; major radius 1) */
     const int32_t* csg_op;       /* optional per object: RR_CSG_* (CSG objects; their two children,
                                     left then right, are the group child lists) */
     /* ABI 4: Perturbed / Noise patterns (pattern.rs:16-19); pat_scale is their scale, pat_a the

@@ -29,7 +29,8 @@ _I = C.POINTER(C.c_int)
 class OrcStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "rays", "shadow_rays", "sphere_tests", "plane_tests", "tri_tests", "group_tests",
-        "group_hits", "cube_tests", "cyl_tests", "cone_tests", "csg_tests", "shade_events", "nan_sorts")]
+        "group_hits", "cube_tests", "cyl_tests", "cone_tests", "csg_tests", "shade_events", "nan_sorts",
+        "torus_tests")]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
@@ -68,6 +69,10 @@ def _load():
         L.orc_add_texture.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]
         L.orc_texture_color.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, C.POINTER(C.c_uint8)]
         L.orc_uv_mapping.argtypes = [C.c_void_p, C.c_int, _D, _D]
+        for n, k in (("quartic", 5), ("cubic", 4), ("quadratic", 3)):
+            f = getattr(L, "orc_find_roots_" + n)
+            f.argtypes = [C.c_double] * k + [_D]
+            f.restype = C.c_int
         L.orc_pattern_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_double),
                                        C.POINTER(C.c_int64)]
         L.orc_get_inverse.argtypes = [C.c_void_p, C.c_int, _D]
@@ -197,7 +202,7 @@ DEFAULT_MAT7 = (0.1, 0.9, 0.9, 200.0, 0.0, 0.0, 1.0)  # material.rs:47-58
 PAT = {"test": 0, "solid": 1, "stripe": 2, "gradient": 3, "ring": 4, "checker": 5, "blend": 6, "perturbed": 7,
        "noise": 8, "texture": 9}
 KIND = {"sphere": 0, "plane": 1, "group": 2, "triangle": 3, "smooth_triangle": 4, "cube": 5, "cylinder": 6,
-        "cone": 7, "csg": 8}
+        "cone": 7, "csg": 8, "torus": 9}
 CSG_OP = {"union": 0, "intersection": 1, "difference": 2}  # csg.rs:13-17
 
 
@@ -312,6 +317,15 @@ class Oracle:
         out = (C.c_double * 2)()
         self.L.orc_uv_mapping(self.w, oid, _dv(p), out)
         return out[0], out[1]
+
+    @staticmethod
+    def find_roots(*coeffs):
+        """roots 0.0.8 find_roots_{quadratic,cubic,quartic} by the number of coefficients."""
+        L = _load()
+        f = {3: L.orc_find_roots_quadratic, 4: L.orc_find_roots_cubic, 5: L.orc_find_roots_quartic}[len(coeffs)]
+        out = (C.c_double * 4)()
+        n = f(*[float(c) for c in coeffs], out)
+        return [out[i] for i in range(n)]
 
     def num_patterns(self):
         return self.L.orc_num_patterns(self.w)

@@ -339,6 +339,247 @@ Tuple normal_to_world(const orc_world* w, int id, const Tuple& n) {
     return nn;
 }
 
+// ---------------------------------------------------------------- roots 0.0.8 (crates.io "roots")
+// torus.rs calls roots::find_roots_quartic; the crate is a third-party dependency (Cargo.toml:18,
+// roots = "0.0.8") not vendored in the reference.  Restated from its published analytical solvers
+// (src/analytical/{linear,quadratic,biquadratic,cubic,cubic_depressed,cubic_normalized,quartic,
+// quartic_depressed}.rs): Roots<F> keeps its roots ascending, and add_new_root drops a value equal
+// to one already present.  Parity of this restatement is pinned only through the reference's own
+// rendered example1.png (tests/test_oracle_png.py).
+namespace rootsq {
+struct Roots {
+    int n = 0;
+    double v[4];
+};
+Roots add_new_root(Roots r, double x) {
+    int pos = 0;
+    for (int i = 0; i < r.n; ++i) {
+        if (r.v[i] == x) return r;
+        if (r.v[i] > x) break;
+        pos++;
+    }
+    if (r.n >= 4) return r;
+    for (int i = r.n; i > pos; --i) r.v[i] = r.v[i - 1];
+    r.v[pos] = x;
+    r.n++;
+    return r;
+}
+Roots one(double x) {
+    Roots r;
+    r.n = 1;
+    r.v[0] = x;
+    return r;
+}
+const double FRAC_PI_3 = 1.04719755119659774615421446109316763;
+const double TWO_THIRD_PI = 2.0 * FRAC_PI_3;
+
+Roots linear(double a1, double a0) {  // linear.rs
+    if (a1 == 0.0) return a0 == 0.0 ? one(0.0) : Roots{};
+    return one(-a0 / a1);
+}
+Roots quadratic(double a2, double a1, double a0) {  // quadratic.rs
+    if (a2 == 0.0) return linear(a1, a0);
+    double discriminant = a1 * a1 - 4.0 * a2 * a0;
+    if (discriminant < 0.0) return Roots{};
+    double a2x2 = 2.0 * a2;
+    if (discriminant == 0.0) return one(-a1 / a2x2);
+    double sq = std::sqrt(discriminant);
+    double same_sign, diff_sign;
+    if (a1 < 0.0) {
+        same_sign = -a1 + sq;
+        diff_sign = -a1 - sq;
+    } else {
+        same_sign = -a1 - sq;
+        diff_sign = -a1 + sq;
+    }
+    double x1, x2;
+    if (std::fabs(same_sign) > std::fabs(a2x2)) {
+        double a0x2 = 2.0 * a0;
+        if (std::fabs(diff_sign) > std::fabs(a2x2)) {
+            x1 = a0x2 / same_sign;
+            x2 = a0x2 / diff_sign;
+        } else {
+            x1 = a0x2 / same_sign;
+            x2 = same_sign / a2x2;
+        }
+    } else {
+        x1 = diff_sign / a2x2;
+        x2 = same_sign / a2x2;
+    }
+    Roots r;
+    r.n = 2;
+    if (x1 < x2) {
+        r.v[0] = x1;
+        r.v[1] = x2;
+    } else {
+        r.v[0] = x2;
+        r.v[1] = x1;
+    }
+    return r;
+}
+Roots biquadratic(double a4, double a2, double a0) {  // biquadratic.rs
+    if (a4 == 0.0) return quadratic(a2, 0.0, a0);
+    Roots out;
+    Roots q = quadratic(a4, a2, a0);
+    for (int i = 0; i < q.n; ++i) {
+        double x = q.v[i];
+        if (x > 0.0) {
+            double s = std::sqrt(x);
+            out = add_new_root(add_new_root(out, -s), s);
+        } else if (x == 0.0) {
+            out = add_new_root(out, 0.0);
+        }
+    }
+    return out;
+}
+Roots cubic_normalized(double a2, double a1, double a0) {  // cubic_normalized.rs: x^3 + a2 x^2 + a1 x + a0
+    double q = (3.0 * a1 - a2 * a2) / 9.0;
+    double r = (9.0 * a2 * a1 - 27.0 * a0 - 2.0 * a2 * a2 * a2) / 54.0;
+    double q3 = q * q * q;
+    double d = q3 + r * r;
+    double a2_div_3 = a2 / 3.0;
+    if (d < 0.0) {
+        double phi_3 = std::acos(r / std::sqrt(-q3)) / 3.0;
+        double sqrt_q_2 = 2.0 * std::sqrt(-q);
+        Roots out = one(sqrt_q_2 * std::cos(phi_3) - a2_div_3);
+        out = add_new_root(out, sqrt_q_2 * std::cos(phi_3 - TWO_THIRD_PI) - a2_div_3);
+        return add_new_root(out, sqrt_q_2 * std::cos(phi_3 + TWO_THIRD_PI) - a2_div_3);
+    }
+    double sqrt_d = std::sqrt(d);
+    double s = std::cbrt(r + sqrt_d);
+    double t = std::cbrt(r - sqrt_d);
+    if (s == t) {
+        if (s + t == 0.0) return one(s + t - a2_div_3);
+        return add_new_root(one(s + t - a2_div_3), -(s + t) / 2.0 - a2_div_3);
+    }
+    return one(s + t - a2_div_3);
+}
+Roots cubic_depressed(double a1, double a0) {  // cubic_depressed.rs: x^3 + a1 x + a0
+    if (a1 == 0.0) return one(-std::cbrt(a0));
+    if (a0 == 0.0) return add_new_root(quadratic(1.0, 0.0, a1), 0.0);
+    double d = a0 * a0 / 4.0 + a1 * a1 * a1 / 27.0;
+    if (d < 0.0) {
+        double a = std::sqrt(-4.0 * a1 / 3.0);
+        double phi = std::acos(-4.0 * a0 / (a * a * a)) / 3.0;
+        Roots out = one(a * std::cos(phi));
+        out = add_new_root(out, a * std::cos(phi + TWO_THIRD_PI));
+        return add_new_root(out, a * std::cos(phi - TWO_THIRD_PI));
+    }
+    double sqrt_d = std::sqrt(d);
+    double a0_div_2 = a0 / 2.0;
+    double x1 = std::cbrt(sqrt_d - a0_div_2) - std::cbrt(sqrt_d + a0_div_2);
+    if (d == 0.0) return add_new_root(one(x1), std::cbrt(a0_div_2));
+    return one(x1);
+}
+Roots cubic(double a3, double a2, double a1, double a0) {  // cubic.rs
+    if (a3 == 0.0) return quadratic(a2, a1, a0);
+    if (a2 == 0.0) return cubic_depressed(a1 / a3, a0 / a3);
+    if (a3 == 1.0) return cubic_normalized(a2, a1, a0);
+    double d = 18.0 * a3 * a2 * a1 * a0 - 4.0 * a2 * a2 * a2 * a0 + a2 * a2 * a1 * a1 - 4.0 * a3 * a1 * a1 * a1 -
+               27.0 * a3 * a3 * a0 * a0;
+    double d0 = a2 * a2 - 3.0 * a3 * a1;
+    double d1 = 2.0 * a2 * a2 * a2 - 9.0 * a3 * a2 * a1 + 27.0 * a3 * a3 * a0;
+    if (d < 0.0) {  // one real root
+        double sq = std::sqrt(-27.0 * a3 * a3 * d);
+        double c = std::cbrt((d1 < 0.0 ? d1 - sq : d1 + sq) / 2.0);
+        return one(-(a2 + c + d0 / c) / (3.0 * a3));
+    }
+    if (d == 0.0) {
+        if (d0 == 0.0) return one(-a2 / (a3 * 3.0));  // triple root
+        return add_new_root(one((9.0 * a3 * a0 - a2 * a1) / (d0 * 2.0)),
+                            (4.0 * a3 * a2 * a1 - 9.0 * a3 * a3 * a0 - a2 * a2 * a2) / (a3 * d0));
+    }
+    // three real roots through the complex cube root of (d1 + i sqrt(27 a3^2 d)) / 2
+    double c3_img = std::sqrt(27.0 * a3 * a3 * d) / 2.0;
+    double c3_real = d1 / 2.0;
+    double c3_module = std::sqrt(c3_img * c3_img + c3_real * c3_real);
+    double c3_phase = 2.0 * std::atan(c3_img / (c3_real + c3_module));
+    double c_module = std::cbrt(c3_module);
+    double c_phase = c3_phase / 3.0;
+    double c_real = c_module * std::cos(c_phase);
+    double c_img = c_module * std::sin(c_phase);
+    double x0_real = -(a2 + c_real + (d0 * c_real) / (c_module * c_module)) / (3.0 * a3);
+    double e_real = -1.0 / 2.0;
+    double e_img = std::sqrt(3.0) / 2.0;
+    double c1_real = c_real * e_real - c_img * e_img;
+    double c1_img = c_real * e_img + c_img * e_real;
+    double x1_real = -(a2 + c1_real + (d0 * c1_real) / (c1_real * c1_real + c1_img * c1_img)) / (3.0 * a3);
+    double c2_real = c1_real * e_real - c1_img * e_img;
+    double c2_img = c1_real * e_img + c1_img * e_real;
+    double x2_real = -(a2 + c2_real + (d0 * c2_real) / (c2_real * c2_real + c2_img * c2_img)) / (3.0 * a3);
+    return add_new_root(add_new_root(one(x0_real), x1_real), x2_real);
+}
+Roots quartic_depressed(double a2, double a1, double a0) {  // quartic_depressed.rs: x^4 + a2 x^2 + a1 x + a0
+    if (a1 == 0.0) return biquadratic(1.0, a2, a0);
+    if (a0 == 0.0) return add_new_root(cubic_normalized(0.0, a2, a1), 0.0);
+    // resolvent y^3 + 5/2 a2 y^2 + (2 a2^2 - a0) y + (a2^3 - a2 a0 - a1^2 / 4) / 2, largest root
+    double a2_pow_2 = a2 * a2;
+    double a1_div_2 = a1 / 2.0;
+    double b2 = a2 * 5.0 / 2.0;
+    double b1 = 2.0 * a2_pow_2 - a0;
+    double b0 = (a2_pow_2 * a2 - a2 * a0 - a1_div_2 * a1_div_2) / 2.0;
+    Roots res = cubic_normalized(b2, b1, b0);
+    double y = res.v[res.n - 1];
+    double a2_plus_2y = a2 + 2.0 * y;
+    if (!(a2_plus_2y > 0.0)) return Roots{};
+    double sqrt_a2_plus_2y = std::sqrt(a2_plus_2y);
+    double q0a = a2 + y - a1_div_2 / sqrt_a2_plus_2y;
+    double q0b = a2 + y + a1_div_2 / sqrt_a2_plus_2y;
+    Roots out = quadratic(1.0, sqrt_a2_plus_2y, q0a);
+    Roots more = quadratic(1.0, -sqrt_a2_plus_2y, q0b);
+    for (int i = 0; i < more.n; ++i) out = add_new_root(out, more.v[i]);
+    return out;
+}
+// quartic.rs: depressed quartic y^4 + p y^2 + q y + r with x = y - a3 / (4 a4)
+Roots via_depressed_quartic(double a4, double a3, double a2, double a1, double a0, double pp, double rr, double dd) {
+    double a4_pow_2 = a4 * a4;
+    double a4_pow_3 = a4_pow_2 * a4;
+    double a4_pow_4 = a4_pow_2 * a4_pow_2;
+    double p = pp / (8.0 * a4_pow_2);
+    double q = rr / (8.0 * a4_pow_3);
+    double r = (dd + 16.0 * a4_pow_2 * (12.0 * a0 * a4 - 3.0 * a1 * a3 + a2 * a2)) / (256.0 * a4_pow_4);
+    Roots dep = quartic_depressed(p, q, r);
+    Roots out;
+    for (int i = 0; i < dep.n; ++i) out = add_new_root(out, dep.v[i] - a3 / (4.0 * a4));
+    return out;
+}
+// quartic.rs: the discriminant (partially factored) and P, R, Delta0, D of the nature-of-roots table
+// classify the equation first; only the cases with real roots go through Ferrari's resolvent.
+Roots quartic(double a4, double a3, double a2, double a1, double a0) {
+    if (a4 == 0.0) return cubic(a3, a2, a1, a0);
+    if (a0 == 0.0) return add_new_root(cubic(a4, a3, a2, a1), 0.0);
+    if (a1 == 0.0 && a3 == 0.0) return biquadratic(a4, a2, a0);
+    double discriminant =
+        a4 * a0 * a4 * (256.0 * a4 * a0 * a0 + a1 * (144.0 * a2 * a1 - 192.0 * a3 * a0)) +
+        a4 * a0 * a2 * a2 * (16.0 * a2 * a2 - 80.0 * a3 * a1 - 128.0 * a4 * a0) +
+        (a3 * a3 *
+         (a4 * a0 * (144.0 * a2 * a0 - 6.0 * a1 * a1) +
+          (a0 * (18.0 * a3 * a2 * a1 - 27.0 * a3 * a3 * a0 - 4.0 * a2 * a2 * a2) + a1 * a1 * (a2 * a2 - 4.0 * a3 * a1)))) +
+        a4 * a1 * a1 * (18.0 * a3 * a2 * a1 - 27.0 * a4 * a1 * a1 - 4.0 * a2 * a2 * a2);
+    double pp = 8.0 * a4 * a2 - 3.0 * a3 * a3;
+    double rr = a3 * a3 * a3 + 8.0 * a4 * a4 * a1 - 4.0 * a4 * a3 * a2;
+    double delta0 = a2 * a2 - 3.0 * a3 * a1 + 12.0 * a4 * a0;
+    double dd = 64.0 * a4 * a4 * a4 * a0 - 16.0 * a4 * a4 * a2 * a2 + 16.0 * a4 * a3 * a3 * a2 -
+                16.0 * a4 * a4 * a3 * a1 - 3.0 * a3 * a3 * a3 * a3;
+    if (discriminant == 0.0) {
+        bool triple_root = delta0 == 0.0;
+        bool quadruple_root = triple_root && dd == 0.0;
+        bool no_roots = dd == 0.0 && pp > 0.0 && rr == 0.0;
+        if (quadruple_root) return one(-a3 / (4.0 * a4));
+        if (triple_root) {
+            double x0 = (-72.0 * a4 * a4 * a0 + 10.0 * a4 * a2 * a2 - 3.0 * a3 * a3 * a2) /
+                        (9.0 * (8.0 * a4 * a4 * a1 - 4.0 * a4 * a3 * a2 + a3 * a3 * a3));
+            return add_new_root(one(x0), -(a3 / a4 + 3.0 * x0));
+        }
+        if (no_roots) return Roots{};
+        return via_depressed_quartic(a4, a3, a2, a1, a0, pp, rr, dd);
+    }
+    bool no_roots = discriminant > 0.0 && (pp > 0.0 || dd > 0.0);
+    if (no_roots) return Roots{};  // two pairs of complex conjugate roots
+    return via_depressed_quartic(a4, a3, a2, a1, a0, pp, rr, dd);
+}
+}  // namespace rootsq
+
 Tuple local_normal_at(const Object& o, const Tuple& lp, const Intersection& hit) {
     switch (o.kind) {
         case ORC_SPHERE: return sub(lp, point(0.0, 0.0, 0.0));  // sphere.rs:80-82
@@ -365,6 +606,13 @@ Tuple local_normal_at(const Object& o, const Tuple& lp, const Intersection& hit)
             double y = std::sqrt(dist);
             if (lp.y > 0.0) y = -y;
             return vector(lp.x, y, lp.z);
+        }
+        case ORC_TORUS: {  // torus.rs:97-107
+            double sum_squared = lp.x * lp.x + lp.y * lp.y + lp.z * lp.z;
+            double param_squared = 1.0 + o.minimum * o.minimum;
+            Tuple n = vector(4.0 * lp.x * (sum_squared - param_squared), 4.0 * lp.y * (sum_squared - param_squared),
+                             4.0 * lp.z * (sum_squared - param_squared + 2.0));
+            return normalize(n);
         }
         default: return vector(0, 0, 0);  // group.rs: panics ("Groups do not have normals")
     }
@@ -430,6 +678,10 @@ AABB get_aabb(orc_world* w, int id) {
         case ORC_CONE: {                                                          // cone.rs:221-226
             double limit = std::fmax(std::fabs(o.minimum), std::fabs(o.maximum));
             return {point(-limit, o.minimum, -limit), point(limit, o.maximum, limit)};
+        }
+        case ORC_TORUS: {  // torus.rs get_aabb
+            double r = o.minimum;
+            return {point(-1.0 - r, -1.0 - r, -r), point(1.0 + r, 1.0 + r, r)};
         }
         case ORC_CSG:  // csg.rs get_aabb (cached): left then right, transformed
         case ORC_GROUP: {  // group.rs:128-149 (cached)
@@ -614,6 +866,26 @@ void local_intersect(const orc_world* w, int id, const Ray& ray, std::vector<Int
             double y1 = og.y + t1 * d.y;
             if (o.minimum < y1 && y1 < o.maximum) xs.push_back({t1, o.id, 0.0, 0.0});
             caps();
+            return;
+        }
+        case ORC_TORUS: {  // torus.rs:37-95
+            ctx.st.torus_tests++;
+            const Tuple& og = ray.origin;
+            const Tuple& d = ray.direction;
+            double r = o.minimum;
+            double r_sq = r * r;
+            double sum_d_sq = d.x * d.x + d.y * d.y + d.z * d.z;
+            double e = og.x * og.x + og.y * og.y + og.z * og.z - r_sq + 1.0;
+            double f = dot(og, d);
+            const double four = 4.0;
+            double a4 = sum_d_sq * sum_d_sq;
+            double a3 = 4.0 * sum_d_sq * f;
+            double a2 = 2.0 * sum_d_sq * e + 4.0 * f * f - four * (d.x * d.x + d.y * d.y);
+            double a1 = 4.0 * e * f - 2.0 * four * (og.x * d.x + og.y * d.y);
+            double a0 = e * e - four * (og.x * og.x + og.y * og.y);
+            rootsq::Roots rs = rootsq::quartic(a4, a3, a2, a1, a0);
+            for (int i = 0; i < rs.n; ++i)
+                if (rs.v[i] > 0.0) xs.push_back({rs.v[i], o.id, 0.0, 0.0});
             return;
         }
         case ORC_CSG: {  // csg.rs:105-113: left.intersect ++ right.intersect, sort, filter
@@ -874,6 +1146,12 @@ void uv_mapping(const Object& o, const Tuple& p, double& u, double& v) {
             double denom = d00 * d11 - d01 * d01;
             u = (d11 * d20 - d01 * d21) / denom;
             v = (d00 * d21 - d01 * d20) / denom;
+            return;
+        }
+        case ORC_TORUS: {  // torus.rs:150-161
+            u = (std::atan2(p.y, p.x) + PI) / (2.0 * PI);
+            double dist_to_center = std::sqrt(p.x * p.x + p.y * p.y) - 1.0;
+            v = (std::atan2(p.z, dist_to_center) + PI) / (2.0 * PI);
             return;
         }
         default:
@@ -1366,6 +1644,19 @@ int orc_add_texture(orc_world* w, int width, int height, const uint8_t* rgba) {
 void orc_texture_color(orc_world* w, int tex, double u, double v, uint8_t out[4]) {
     texture_color(w->textures[tex], u, v, out);
 }
+static int roots_out(const rootsq::Roots& r, double out[4]) {
+    for (int i = 0; i < r.n; ++i) out[i] = r.v[i];
+    return r.n;
+}
+int orc_find_roots_quartic(double a4, double a3, double a2, double a1, double a0, double out[4]) {
+    return roots_out(rootsq::quartic(a4, a3, a2, a1, a0), out);
+}
+int orc_find_roots_cubic(double a3, double a2, double a1, double a0, double out[4]) {
+    return roots_out(rootsq::cubic(a3, a2, a1, a0), out);
+}
+int orc_find_roots_quadratic(double a2, double a1, double a0, double out[4]) {
+    return roots_out(rootsq::quadratic(a2, a1, a0), out);
+}
 void orc_uv_mapping(orc_world* w, int obj, const double p[3], double out[2]) {
     uv_mapping(w->objects[obj], tp(p, 1.0), out[0], out[1]);
 }
@@ -1489,6 +1780,7 @@ int orc_render(orc_world* w, const orc_camera* c, int max_depth, uint64_t seed, 
             s.csg_tests += x.csg_tests;
             s.shade_events += x.shade_events;
             s.nan_sorts += x.nan_sorts;
+            s.torus_tests += x.torus_tests;
         }
         *stats = s;
     }

@@ -33,7 +33,8 @@ enum { ORC_PAT_TEST = 0, ORC_PAT_SOLID = 1, ORC_PAT_STRIPE = 2, ORC_PAT_GRADIENT
        ORC_PAT_TEXTURE = 9 /* a = texture id */ };
 /* object kinds */
 enum { ORC_SPHERE = 0, ORC_PLANE = 1, ORC_GROUP = 2, ORC_TRIANGLE = 3, ORC_SMOOTH_TRIANGLE = 4,
-       ORC_CUBE = 5, ORC_CYLINDER = 6, ORC_CONE = 7, ORC_CSG = 8 };
+       ORC_CUBE = 5, ORC_CYLINDER = 6, ORC_CONE = 7, ORC_CSG = 8,
+       ORC_TORUS = 9 /* minor radius = shape param `minimum` */ };
 /* CSG operations (csg.rs:13-17) */
 enum { ORC_CSG_UNION = 0, ORC_CSG_INTERSECTION = 1, ORC_CSG_DIFFERENCE = 2 };
 
@@ -44,6 +45,7 @@ typedef struct {
     uint64_t cube_tests, cyl_tests, cone_tests, csg_tests;
     uint64_t shade_events;  /* shade_hit calls */
     uint64_t nan_sorts;     /* sort comparisons that would panic in the reference */
+    uint64_t torus_tests;
 } orc_stats;
 
 /* ---- matrices (matrix.rs) — 4x4 row-major double[16] ---- */
@@ -115,6 +117,10 @@ int  orc_add_texture(orc_world* w, int width, int height, const uint8_t* rgba);
 void orc_texture_color(orc_world* w, int tex, double u, double v, uint8_t out[4]);
 /* Object::uv_mapping of object `obj` at an object-space point */
 void orc_uv_mapping(orc_world* w, int obj, const double p[3], double out[2]);
+/* roots 0.0.8 find_roots_quartic(a4, a3, a2, a1, a0): returns the number of roots (0-4), ascending */
+int  orc_find_roots_quartic(double a4, double a3, double a2, double a1, double a0, double out[4]);
+int  orc_find_roots_cubic(double a3, double a2, double a1, double a0, double out[4]);
+int  orc_find_roots_quadratic(double a2, double a1, double a0, double out[4]);
 void orc_normal_at(orc_world* w, int obj, const double p[3], double u, double v, double out[4]);
 void orc_world_to_object(orc_world* w, int obj, const double p[3], double out[4]);
 void orc_normal_to_world(orc_world* w, int obj, const double n[3], double out[4]);

@@ -225,8 +225,9 @@ class YamlSceneBuilder:
             oid = o.add_csg(op, parent)
             self.create_shape(_get(s, "left"), oid)
             self.create_shape(_get(s, "right"), oid)
-        elif ty == "torus":
-            raise NotImplementedError(f"shape '{ty}' is out of scope (SURVEY.md §8 next-4)")
+        elif ty == "torus":  # :350-353
+            oid = o.add("torus", parent)
+            o.set_shape_params(oid, get_f64(_get(s, "minor_radius")), math.inf, False)
         else:
             raise ValueError(f"Unknown object type: {ty}")
         ts = _get(s, "transforms")

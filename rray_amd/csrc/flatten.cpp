@@ -378,13 +378,26 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
             return RR_E_NONAFFINE;
         }
         int k = d.kind[i];
-        if (k < RR_SPHERE || k > RR_CSG) {
+        if (k < RR_SPHERE || k > RR_TORUS) {
             err = "unknown object kind";
             return RR_E_ARG;
         }
         if (k == RR_CSG && (d.child_count ? d.child_count[i] : 0) != 2) {
             err = "CSG object " + std::to_string(i) + " needs exactly a left and a right child";
             return RR_E_SCENE;  // csg.rs: get_object(usize::MAX) panics
+        }
+        if (k == RR_TORUS) {  // torus.rs:23-31: minor radius (major radius 1)
+            if (!d.shape) {
+                err = "torus without its minor radius (rr_scene_desc.shape)";
+                return RR_E_ARG;
+            }
+            DevShape s{};
+            s.minimum = d.shape[3 * (size_t)i];
+            s.maximum = 0.0;
+            s.closed = 0;
+            tri_index[i] = (int)out.shapes.size();
+            out.shapes.push_back(s);
+            out.has_quad = 1;
         }
         if (k == RR_CYLINDER || k == RR_CONE) {  // cylinder.rs:29-37, cone.rs:30-38
             DevShape s{};
@@ -438,6 +451,10 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
             if (k == RR_CYLINDER) return {point(-1, s.minimum, -1), point(1, s.maximum, 1)};  // cylinder.rs
             double limit = std::fmax(std::fabs(s.minimum), std::fabs(s.maximum));             // cone.rs:221-226
             return {point(-limit, s.minimum, -limit), point(limit, s.maximum, limit)};
+        }
+        if (k == RR_TORUS) {  // torus.rs get_aabb
+            const double r = out.shapes[tri_index[id]].minimum;
+            return {point(-1.0 - r, -1.0 - r, -r), point(1.0 + r, 1.0 + r, r)};
         }
         if (!is_container(k)) {                                                    // triangle.rs get_aabb
             const double* p = d.tri + 18 * (size_t)id;
@@ -625,7 +642,10 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
                 const int self = (int)(&nd - out.nodes.data());
                 for (int j = self + 1; j < nd.skip; ++j)
                     if (!is_container(out.nodes[j].kind))
-                        entries += (out.nodes[j].kind == RR_CYLINDER || out.nodes[j].kind == RR_CONE) ? 4 : 2;
+                        entries += (out.nodes[j].kind == RR_CYLINDER || out.nodes[j].kind == RR_CONE ||
+                                    out.nodes[j].kind == RR_TORUS)
+                                       ? 4
+                                       : 2;
                 if (entries > RR_MAX_CSG_ENTRIES) {
                     err = "a CSG subtree can produce more than RR_MAX_CSG_ENTRIES intersections";
                     return RR_E_LIMIT;

@@ -326,8 +326,10 @@ struct Builder {
             S.csg_op[id] = code;
             create_shape(s["left"], id);
             create_shape(s["right"], id);
-        } else if (t == "torus") {
-            panic("shape 'torus' is outside the GPU path's scope (SURVEY.md §8 next-4)", RR_E_LIMIT);
+        } else if (t == "torus") {  // :350-353
+            const double r = get_f64(s["minor_radius"]);
+            id = new_object(RR_TORUS, parent);
+            S.shape[3 * (size_t)id] = r;
         } else {
             panic("Unknown object type: " + t);
         }

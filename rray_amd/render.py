@@ -114,6 +114,12 @@ class SceneBuilder:
         self.csg_op[oid] = _lib.CSG_OPS[op] if isinstance(op, str) else int(op)
         return oid
 
+    def torus(self, minor_radius, transform=None, material=None, pattern=-1, parent=-1):
+        """Torus in the xy plane, major radius 1 (torus.rs:23-31)."""
+        oid = self._obj(_lib.TORUS, parent, transform, material, pattern)
+        self.shape[3 * oid] = float(minor_radius)
+        return oid
+
     def triangle(self, p1, p2, p3, transform=None, material=None, pattern=-1, parent=-1):
         return self._obj(_lib.TRIANGLE, parent, transform, material, pattern, list(p1) + list(p2) + list(p3) + [0.0] * 9)
 

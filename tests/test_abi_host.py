@@ -62,7 +62,8 @@ YAMLS = [(SCENES, f) for f in ("c1_readme.yaml", "c2_s1024.yaml", "c3_s1024_refl
                                "ring_pattern.yaml", "blend_pattern.yaml", "triangle.yaml", "objects_cylinder.yaml",
                                "objects_cone.yaml", "shapes_csg.yaml", "shapes_glass.yaml", "shapes_mixed.yaml",
                                "noise_pattern.yaml", "perturbed_pattern.yaml", "objects_sphere.yaml",
-                               "objects_cube.yaml", "patterns_noise_mix.yaml", "textures_mix.yaml")]
+                               "objects_cube.yaml", "patterns_noise_mix.yaml", "textures_mix.yaml",
+                               "shapes_torus.yaml")] + [(os.path.join(GOLDEN, "example1"), "example1.yaml")]
 
 
 @pytest.mark.parametrize("root,name", YAMLS)
@@ -84,6 +85,8 @@ def test_yaml_front_end_matches_oracle_builder(R, oracle_mod, root, name):
             assert np.array_equal(aabb[i], np.array(o.group_aabb(i)), equal_nan=True), (name, i)
         if d.kind[i] in (6, 7):  # cylinder / cone parameters
             assert [d.shape[3 * i + k] for k in range(3)] == o.shape_params(i), (name, i)
+        if d.kind[i] == 9:  # torus minor radius
+            assert d.shape[3 * i] == o.shape_params(i)[0], (name, i)
         if d.kind[i] == 8:
             assert d.csg_op[i] == o.csg_op(i), (name, i)
     assert d.n_patterns == o.num_patterns()
@@ -113,10 +116,13 @@ def test_yaml_edge_cases(R):
         R.YamlScene(base + "lights: []\rscene: []\r", 10, 10, 1)  # "No lights found in scene"
     with pytest.raises(R.RRError):
         R.YamlScene(base + "lights:\r  - type: spot\r    color: [1,1,1]\rscene: []\r", 10, 10, 1)
-    with pytest.raises(R.RRError) as e:
-        R.YamlScene(base + "lights:\r  - type: point\r    color: [1,1,1]\r    position: [0,0,0]\r"
+    s = R.YamlScene(base + "lights:\r  - type: point\r    color: [1,1,1]\r    position: [0,0,0]\r"
                     "scene:\r  - type: torus\r    minor_radius: 0.25\r", 10, 10, 1)
-    assert e.value.code == -5  # RR_E_LIMIT: out-of-scope shape (next-4), reported not silently dropped
+    assert s.desc().kind[0] == R._lib.TORUS and s.desc().shape[0] == 0.25
+    with pytest.raises(R.RRError) as e:  # torus.rs: minor_radius is required (get_f64 panics)
+        R.YamlScene(base + "lights:\r  - type: point\r    color: [1,1,1]\r    position: [0,0,0]\r"
+                    "scene:\r  - type: torus\r", 10, 10, 1)
+    assert e.value.code == R._lib.RR_E_SCENE
     lights = "lights:\r  - type: point\r    color: [1,1,1]\r    position: [0,0,0]\r"
     with pytest.raises(R.RRError) as e:
         s = R.YamlScene(base + lights + "scene:\r  - type: sphere\r    material:\r      pattern:\r        type: noise\r"
@@ -219,3 +225,6 @@ def test_png_texture_decoder_matches_pil(R):
     with pytest.raises(R.RRError) as e:
         R.YamlScene(text.replace("tex_grid.png", "missing.png"), 8, 8, 1, obj_root=GOLDEN)
     assert e.value.code == R._lib.RR_E_IO
+    with pytest.raises(R.RRError) as e:  # JPEG (examples/Texturelabs_Stone_138M.jpg): host-side decode only
+        R.YamlScene(text.replace("png/tex_grid.png", "teapot-low.obj"), 8, 8, 1, obj_root=GOLDEN)
+    assert e.value.code == R._lib.RR_E_LIMIT

@@ -106,7 +106,8 @@ def test_reference_example_scenes(renderer, name):
                                          ("objects_cone.yaml", 48, 24, 1), ("patterns_noise_mix.yaml", 64, 32, 2),
                                          ("noise_pattern.yaml", 64, 32, 1), ("perturbed_pattern.yaml", 64, 32, 1),
                                          ("objects_sphere.yaml", 48, 24, 2), ("textures_mix.yaml", 96, 48, 2),
-                                         ("textures_mix.yaml", 200, 100, 1)])
+                                         ("textures_mix.yaml", 200, 100, 1), ("shapes_torus.yaml", 96, 48, 2),
+                                         ("shapes_torus.yaml", 200, 100, 1)])
 def test_shape_scenes(renderer, name, W, H, aa):
     """Cube / cylinder / cone / CSG through the general kernel variant: 4-entry
     leaves, CSG subtrees evaluated per lane, n1/n2 over filtered entries.  Perturbed / noise
@@ -142,6 +143,22 @@ def test_reference_png_through_gpu(renderer, R, name, png, aa):
     ref = np.asarray(PIL.open(os.path.join(GOLDEN, "png", png)).convert("RGB"))
     diff = int((q != ref).any(axis=2).sum())
     print(f"{png}: {diff} of {ref.shape[0] * ref.shape[1]} pixels differ")
+    assert diff == 0
+
+
+def test_example1_png_through_gpu(renderer, R):
+    """The reference's headline image (README example1.png, 800x400, aa=3): torus (roots 0.0.8
+    quartic), earthmap texture, noise / perturbed, CSG, cube / cylinder / cone, the full teapot."""
+    PIL = pytest.importorskip("PIL.Image")
+    root = os.path.join(GOLDEN, "example1")
+    text = open(os.path.join(root, "example1.yaml")).read()
+    scene = R.YamlScene(text, 800, 400, 3, obj_root=root)
+    renderer.upload(scene)
+    avg = renderer.render(scene.camera, aa=3, max_depth=5)["avg"]
+    q = R.quantize(avg)[..., :3]
+    ref = np.asarray(PIL.open(os.path.join(root, "example1.png")).convert("RGB"))
+    diff = int((q != ref).any(axis=2).sum())
+    print(f"example1.png: {diff} of {ref.shape[0] * ref.shape[1]} pixels differ")
     assert diff == 0
 
 

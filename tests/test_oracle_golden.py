@@ -492,3 +492,44 @@ def test_perlin_properties(oracle_mod):
     assert math.isnan(lib.orc_octave_perlin(1.0, 2.0, 3.0, 0, 0.5))
     x = lib.orc_octave_perlin(10.0, 20.0, 30.0, 1, 0.5)
     assert x == lib.orc_noise_3d(10.0, 20.0, 30.0)
+
+
+def test_roots_quartic_solver(oracle_mod):
+    """roots 0.0.8 find_roots_* as restated for torus.rs (third-party, not vendored: properties of the
+    published algorithm; the values are pinned through example1.png in test_oracle_png.py)."""
+    f = oracle_mod.Oracle.find_roots
+    r = f(1.0, -10.0, 35.0, -50.0, 24.0)  # (x-1)(x-2)(x-3)(x-4)
+    assert len(r) == 4 and all(abs(a - b) < 1e-9 for a, b in zip(r, [1, 2, 3, 4]))
+    assert f(1.0, 0.0, 0.0, 0.0, 1.0) == []         # x^4 + 1: biquadratic, no real roots
+    assert f(1.0, 0.0, -5.0, 0.0, 4.0) == [-2.0, -1.0, 1.0, 2.0]  # biquadratic branch, exact
+    assert f(1.0, 2.0, 3.0, 4.0, 0.0)[-1] == 0.0 or 0.0 in f(1.0, 2.0, 3.0, 4.0, 0.0)  # a0 = 0: zero root
+    assert f(1.0, 4.0, 10.0, 12.0, 9.0) == []       # (x^2+2x+3)^2: complex pairs (discriminant 0, no roots)
+    assert f(1.0, -3.0, 2.0) == [1.0, 2.0]           # quadratic, ascending
+    assert f(1.0, -2.0, 1.0) == [1.0]                # double root reported once
+    assert f(0.0, 2.0, -4.0) == [2.0]                # linear
+    c = f(1.0, -6.0, 11.0, -6.0)                    # cubic (x-1)(x-2)(x-3), normalized branch
+    assert len(c) == 3 and all(abs(a - b) < 1e-12 for a, b in zip(c, [1, 2, 3]))
+    c = f(2.0, -12.0, 22.0, -12.0)                  # same roots through the general complex-root branch
+    assert len(c) == 3 and all(abs(a - b) < 1e-9 for a, b in zip(c, [1, 2, 3]))
+    rng = np.random.default_rng(3)
+    for _ in range(200):  # random real-rooted quartics: every returned value is a root, ascending
+        roots = np.sort(rng.uniform(-5, 5, 4))
+        co = np.poly(roots)
+        got = f(*co)
+        assert got == sorted(got)
+        assert len(got) <= 4
+        for x in got:
+            assert abs(np.polyval(co, x)) < 1e-6 * max(1.0, np.abs(co).max())
+
+
+def test_torus_intersections(oracle_mod):
+    """torus.rs:37-95 through the object API: a ray along +z through the tube hits it twice on each
+    side of the hole (xy-plane torus, major radius 1), none through the hole's centre."""
+    o = oracle_mod.Oracle()
+    t = o.add("torus")
+    o.set_shape_params(t, 0.25, math.inf, False)
+    xs = o.local_intersect(t, (1.0, 0.0, -5.0, 1.0), (0.0, 0.0, 1.0, 0.0))
+    assert [round(x[0], 9) for x in xs] == [4.75, 5.25]
+    assert o.local_intersect(t, (0.0, 0.0, -5.0, 1.0), (0.0, 0.0, 1.0, 0.0)) == []
+    xs = o.local_intersect(t, (-5.0, 0.0, 0.0, 1.0), (1.0, 0.0, 0.0, 0.0))
+    assert [round(x[0], 9) for x in xs] == [3.75, 4.25, 5.75, 6.25]

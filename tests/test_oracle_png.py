@@ -5,7 +5,9 @@ quantises (`as u8`, canvas.rs:76-105), and must reproduce every pixel.  The patt
 rendered with aa=1, the objects scenes with aa=3 (every other aa leaves ~7 % of the edge pixels
 different; aa=3 leaves none).  noise_pattern / perturbed_pattern and objects/sphere, objects/cube
 (blends of noise patterns) pin the fastnoise-lite 1.1.1 Perlin restatement (oracle/rray_oracle.cpp,
-namespace fnl) and noise.rs:octave_perlin.  Texture (image / uv) patterns and torus are next."""
+namespace fnl) and noise.rs:octave_perlin.  example1.png (the README's headline image: torus through
+roots 0.0.8's quartic solver, the earthmap texture, noise, perturbed, CSG, cube / cylinder / cone,
+the full teapot OBJ, reflection and refraction) pins everything at once at aa=3."""
 import os
 
 import numpy as np
@@ -41,3 +43,19 @@ def test_oracle_reproduces_reference_png(oracle_mod, scene, png, aa):
     assert q.shape == ref.shape
     diff = int((q != ref).any(axis=2).sum())
     assert diff == 0, f"{diff} pixels differ from the reference's {png}"
+
+
+def test_oracle_reproduces_example1(oracle_mod):
+    """/root/reference/example1.png (800x400, aa=3) from example1.yaml with its examples/ files."""
+    pytest.importorskip("PIL")
+    from oracle.scene_yaml import build_from_yaml
+
+    root = os.path.join(GOLDEN, "example1")
+    text = open(os.path.join(root, "example1.yaml")).read()
+    o, cam = build_from_yaml(text, 800, 400, 3, obj_root=root)
+    canvas, st = o.render(cam, max_depth=5, threads=min(8, os.cpu_count() or 1))
+    assert st["torus_tests"] > 0
+    q = o.quantize(o.aa_average(canvas, 3))[..., :3]
+    ref = _png_rgb(os.path.join(root, "example1.png"))
+    diff = int((q != ref).any(axis=2).sum())
+    assert diff == 0, f"{diff} pixels differ from the reference's example1.png"
