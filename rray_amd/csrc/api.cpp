@@ -70,6 +70,11 @@ struct rr_ctx {
     std::vector<DBuf> comb, pend;  // one per level
     unsigned int* h_lcount = nullptr;  // pinned
     unsigned long long* h_counters = nullptr;
+    // counters: [frame buffer 0][frame buffer 1][queries]; frames alternate (`epoch`), and each
+    // frame's first kernels zero the other buffer for the next frame
+    int epoch = 0;
+    bool zero_next = false;
+    unsigned long long* stats_src = nullptr;  // buffer holding the last frame's counters
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipEvent_t ev_in = nullptr, ev_out = nullptr;
     hipStream_t last_st = nullptr;  // stream of the last render (the context's workspace is ordered on it)
@@ -115,6 +120,8 @@ rr::DevCamera dev_camera(const rr_camera* c) {
     for (int i = 0; i < 16; ++i) t.m[i] = c->transform[i];
     rr::M4 inv = rr::inverse(t);  // camera.rs:85 (cached inverse, same value)
     for (int i = 0; i < 16; ++i) d.inv[i] = inv.m[i];
+    for (int r = 0; r < 4; ++r)  // camera.rs:86 with the kernel's operation order (no contraction)
+        d.origin[r] = d.inv[4 * r] * 0.0 + d.inv[4 * r + 1] * 0.0 + d.inv[4 * r + 2] * 0.0 + d.inv[4 * r + 3] * 1.0;
     return d;
 }
 
@@ -145,6 +152,9 @@ hipError_t sync_ctx(rr_ctx* c) {
 }
 
 constexpr size_t kCounterBytes = (size_t)rr::RR_CNT_SLOTS * rr::RR_CNT_STRIDE * sizeof(unsigned long long);
+unsigned long long* frame_counters(rr_ctx* c, int k) {
+    return c->counters.as<unsigned long long>() + (size_t)k * rr::RR_CNT_SLOTS * rr::RR_CNT_STRIDE;
+}
 
 int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max_depth, double* out, hipStream_t st,
                void* avg = nullptr, int32_t avg_f32 = 0) {
@@ -170,7 +180,8 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             // no level 1, and no host round trip for the child count
             const bool children_possible = d < max_depth && c->host.has_secondary;
             if (children_possible) HIPCHK(nxt_ev->ensure(2 * n * sizeof(rr::Event)));
-            HIPCHK(hipMemsetAsync(c->lcount.p, 0, rr::LC_COUNT * sizeof(unsigned int), st));
+            if (children_possible || c->host.has_transparent)  // queue counters (appends, n1/n2 list)
+                HIPCHK(hipMemsetAsync(c->lcount.p, 0, rr::LC_COUNT * sizeof(unsigned int), st));
             rr::LevelArgs A = base_args;
             A.base = base;
             A.level = d;
@@ -188,7 +199,8 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             A.pending = c->pend[d].as<int32_t>();
             A.n1n2_list = c->n1n2.as<int32_t>();
             A.lcount = c->lcount.as<unsigned int>();
-            A.counters = c->counters.as<unsigned long long>();
+            A.counters = frame_counters(c, c->epoch);
+            A.counters_zero = (c->zero_next && d == 0 && base == 0) ? frame_counters(c, c->epoch ^ 1) : nullptr;
             A.stamps = nullptr;
 #ifdef RR_STAMPS
             // experiment builds: per-wave phase timers of level 0 of the first batch -> $RRAY_STAMPS
@@ -287,7 +299,8 @@ int finish_stats(rr_ctx* c) {
     HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
     // the counters of the last render stay in HBM until the next one zeroes them: copy on demand
     // (a per-frame device-to-host copy behind a cross-stream wait blocks the host in HIP)
-    HIPCHK(hipMemcpy(c->h_counters, c->counters.p, kCounterBytes, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(c->h_counters, c->stats_src ? c->stats_src : frame_counters(c, c->epoch), kCounterBytes,
+                     hipMemcpyDeviceToHost));
     collect_stats(c, &c->last);
     c->last.kernel_ms = ms;
     c->stats_pending = false;
@@ -331,7 +344,8 @@ int rr_create(int device, rr_ctx** out) {
     if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_lcount, 64 * sizeof(unsigned int), hipHostMallocDefault);
     if (e == hipSuccess)
         e = hipHostMalloc((void**)&c->h_counters, kCounterBytes, hipHostMallocDefault);
-    if (e == hipSuccess) e = c->counters.ensure(kCounterBytes);
+    if (e == hipSuccess) e = c->counters.ensure(3 * kCounterBytes);
+    if (e == hipSuccess) e = hipMemset(c->counters.p, 0, 3 * kCounterBytes);
     if (e == hipSuccess) e = c->lcount.ensure(64 * sizeof(unsigned int));
     if (e != hipSuccess) {
         rr_destroy(c);
@@ -498,7 +512,6 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
         HIPCHK(c->canvas.ensure(std::max<int64_t>(total, 1) * 3 * sizeof(double)));
         canvas = c->canvas.as<double>();
     }
-    HIPCHK(hipMemsetAsync(c->counters.p, 0, kCounterBytes, st));
     HIPCHK(hipEventRecord(c->e0, st));
     rr::LevelArgs A{};
     A.cam = dev_camera(cam);
@@ -512,8 +525,12 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     A.seed = o->seed;
     A.jitter_mode = o->jitter_mode;
     const int32_t f32 = (o->flags & RR_OUT_AVG_F32) ? 1 : 0;
+    c->zero_next = true;
     rc = run_levels(c, A, total, o->max_depth, canvas, st, direct_avg ? d_avg : nullptr, f32);
+    c->zero_next = false;
     if (rc != RR_OK) return rc;
+    c->stats_src = frame_counters(c, c->epoch);
+    c->epoch ^= 1;
     if (d_avg && !direct_avg && f32)
         HIPCHK(rr::launch_aa_f32(canvas, static_cast<float*>(d_avg), W, rows, o->aa, st,
                                  c->profile ? &c->prof : nullptr));
@@ -604,7 +621,9 @@ int rr_color_at(rr_ctx* c, int64_t n, const double* origins, const double* direc
         }
     HIPCHK(upload(c->rays0, rays, st));
     HIPCHK(c->qout.ensure(n * 3 * sizeof(double)));
-    HIPCHK(hipMemsetAsync(c->counters.p, 0, kCounterBytes, st));
+    const int saved_epoch = c->epoch;
+    c->epoch = 2;  // the query buffer (frame buffers keep their state)
+    HIPCHK(hipMemsetAsync(frame_counters(c, 2), 0, kCounterBytes, st));
     rr::LevelArgs A{};
     A.hs = 1;
     A.aa = 1;
@@ -615,6 +634,7 @@ int rr_color_at(rr_ctx* c, int64_t n, const double* origins, const double* direc
     A.seed = seed;
     A.jitter_mode = jitter_mode;
     int rc = run_levels(c, A, n, remaining, c->qout.as<double>(), st);
+    c->epoch = saved_epoch;
     if (rc != RR_OK) return rc;
     HIPCHK(hipMemcpyAsync(out_rgb, c->qout.p, n * 3 * sizeof(double), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -634,7 +654,7 @@ int rr_is_shadowed(rr_ctx* c, int64_t n, const double* points, const double* lig
     HIPCHK(upload(c->rays0, buf, st));
     HIPCHK(c->qout.ensure(n * sizeof(int32_t)));
     HIPCHK(rr::launch_shadow_query(c->S, c->rays0.as<double>(), c->rays0.as<double>() + 3 * n, n,
-                                   c->qout.as<int32_t>(), c->counters.as<unsigned long long>(), st));
+                                   c->qout.as<int32_t>(), frame_counters(c, 2), st));
     HIPCHK(hipMemcpyAsync(out, c->qout.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return RR_OK;

@@ -35,6 +35,7 @@ struct LevelArgs {
     uint64_t seed;
     int32_t jitter_mode;
     unsigned long long* counters;  // C_* totals
+    unsigned long long* counters_zero;  // the next frame's counter buffer, zeroed by this frame's kernels (or null)
     unsigned long long* stamps;    // RR_STAMPS experiment builds only: per-wave phase timers (else null)
 };
 

@@ -37,11 +37,9 @@ __device__ __forceinline__ Ray camera_ray(const DevCamera& C, uint32_t px, uint3
     double wx = C.half_width - xoffset;
     double wy = C.half_height - yoffset;
     const double* M = C.inv;
-    double pw[4], ow[4];
-    for (int r = 0; r < 4; ++r) {
-        pw[r] = M[4 * r] * wx + M[4 * r + 1] * wy + M[4 * r + 2] * -1.0 + M[4 * r + 3] * 1.0;
-        ow[r] = M[4 * r] * 0.0 + M[4 * r + 1] * 0.0 + M[4 * r + 2] * 0.0 + M[4 * r + 3] * 1.0;
-    }
+    const double* ow = C.origin;  // M * point(0, 0, 0): pixel-independent, computed on the host
+    double pw[4];
+    for (int r = 0; r < 4; ++r) pw[r] = M[4 * r] * wx + M[4 * r + 1] * wy + M[4 * r + 2] * -1.0 + M[4 * r + 3] * 1.0;
     double dx = pw[0] - ow[0], dy = pw[1] - ow[1], dz = pw[2] - ow[2], dw = pw[3] - ow[3];
     double mag = sqrt(dx * dx + dy * dy + dz * dz + dw * dw);
     return {mk(ow[0], ow[1], ow[2]), mk(dx / mag, dy / mag, dz / mag)};
@@ -53,8 +51,9 @@ __device__ __forceinline__ uint32_t level0_local(const LevelArgs& A, int64_t i) 
     return (A.rays0 || A.lrows <= 0) ? t : tile_to_local_u32(t, (uint32_t)A.hs, (uint32_t)A.lrows);
 }
 
-// the ray of event i at this level; ls = level0_local(A, i) (used at level 0 only)
-__device__ __forceinline__ Ray event_ray(const LevelArgs& A, int64_t i, uint32_t ls) {
+// the ray of event i at this level; ls = level0_local(A, i) (used at level 0 only); camera rays also
+// return their global sample id (the jitter key, as event_key) in s0
+__device__ __forceinline__ Ray event_ray(const LevelArgs& A, int64_t i, uint32_t ls, uint64_t& s0) {
     if (A.level > 0) {
         const Event& e = A.ev[i];
         return {mk(e.o[0], e.o[1], e.o[2]), mk(e.d[0], e.d[1], e.d[2])};
@@ -65,17 +64,22 @@ __device__ __forceinline__ Ray event_ray(const LevelArgs& A, int64_t i, uint32_t
     }
     uint32_t px, py;
     local_to_pixel(A, ls, px, py);
+    s0 = (uint64_t)py * (uint64_t)A.hs + px;
     return camera_ray(A.cam, px, py);
 }
 __device__ __forceinline__ Ray event_ray(const LevelArgs& A, int64_t i) {
-    return event_ray(A, i, A.level > 0 ? 0u : level0_local(A, i));
+    uint64_t s0 = 0;
+    return event_ray(A, i, A.level > 0 ? 0u : level0_local(A, i), s0);
 }
 // jitter identity of event i: (global sample id, recursion path); ls as for event_ray
-__device__ __forceinline__ void event_key(const LevelArgs& A, int64_t i, uint32_t ls0, uint64_t& sample,
+// (s0: event_ray's sample id of a level-0 camera ray)
+__device__ __forceinline__ void event_key(const LevelArgs& A, int64_t i, uint32_t ls0, uint64_t s0, uint64_t& sample,
                                           uint32_t& path) {
     const uint32_t ls = A.level > 0 ? A.ev[i].sample : ls0;
     path = A.level > 0 ? A.ev[i].path : 1u;
-    if (A.rays0) {
+    if (A.level == 0 && !A.rays0) {
+        sample = s0;
+    } else if (A.rays0) {
         sample = (uint64_t)ls;
     } else {
         uint32_t px, py;
@@ -134,8 +138,18 @@ __device__ __forceinline__ bool needs_n1n2(const DevMaterial& m, int rem) {
     return m.transparency != 0.0 && (rem > 0 || m.reflective > 0.0);
 }
 
+// Counters are double-buffered per frame: the first level's kernels clear the buffer the next
+// frame will count into, so no memset sits between frames.
+__device__ __forceinline__ void zero_next_counters(const LevelArgs& A) {
+    if (!A.counters_zero) return;
+    const int total = RR_CNT_SLOTS * RR_CNT_STRIDE;
+    for (int j = (int)(blockIdx.x * blockDim.x + threadIdx.x); j < total; j += (int)(gridDim.x * blockDim.x))
+        A.counters_zero[j] = 0ull;
+}
+
 template <int G, bool LC>
 __global__ void __launch_bounds__(256) trace_kernel(DevScene S, LevelArgs A) {
+    zero_next_counters(A);
     if (LC) stage_culls(S);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < A.n;
@@ -356,8 +370,11 @@ __device__ __forceinline__ void light_step(const DevScene& S, const LevelArgs& A
 // The general variant (G = 2) is not held to 4 waves: squeezed into 128 VGPRs it spills ~300
 // registers, and those builds (ROCm 7.2 clang) returned wrong, run-to-run different images for
 // cube / cylinder / CSG scenes with secondary rays, while every spill-free build is bit-exact.
+#ifndef RR_PRE_WAVES
+#define RR_PRE_WAVES 4
+#endif
 #ifndef RR_SHADE_W3
-#define RR_SHADE_ATTR(PRE, G) __attribute__((amdgpu_waves_per_eu(((PRE) && (G) < 2) ? 4 : 2)))
+#define RR_SHADE_ATTR(PRE, G) __attribute__((amdgpu_waves_per_eu(((PRE) && (G) < 2) ? RR_PRE_WAVES : 2)))
 #else
 #define RR_SHADE_ATTR(PRE, G)
 #endif
@@ -366,6 +383,7 @@ __device__ __forceinline__ void light_step(const DevScene& S, const LevelArgs& A
 // demand (atan2 / acos / Perlin in the callee) otherwise costs the common scenes their occupancy.
 template <int G, bool LC, bool FUSED, bool PRE, bool CP>
 __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevScene S, LevelArgs A) {
+    zero_next_counters(A);
     if (LC) stage_culls(S);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < A.n;
@@ -377,14 +395,20 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
         const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
         cnt.st = w < (1 << 16) ? A.stamps + ((int64_t)(1 << 16) + w) * 8 : nullptr;
     }
+    // FUSED: the (unused) trace region of the stamp buffer takes the shadow walk and extra marks
+    unsigned long long* const st1 = cnt.st;
+    unsigned long long* const st0 = (FUSED && cnt.st) ? cnt.st - (int64_t)(1 << 16) * 8 : nullptr;
     RR_STAMP(cnt, 0);
+#else
+    unsigned long long* const st0 = nullptr;
 #endif
     const uint32_t ls0 = A.level > 0 ? 0u : level0_local(A, i);
     HitRec hr;
     hr.node = -1;
     Ray r0 = {mk(0, 0, 0), mk(0, 0, 1)};  // FUSED: the event's ray, traced here
+    uint64_t s0 = 0;  // level-0 sample id from event_ray
     if (FUSED) {
-        if (valid) r0 = event_ray(A, i, ls0);
+        if (valid) r0 = event_ray(A, i, ls0, s0);
         Hit th;
         trace_closest<G, LC>(S, r0, valid, th, cnt);
         cnt.rays += popc_ballot(valid);
@@ -414,7 +438,7 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
     uint64_t sample = 0;
     uint32_t path = 1u;
     if (has_hit) {
-        const Ray r = FUSED ? r0 : event_ray(A, i, ls0);
+        const Ray r = FUSED ? r0 : event_ray(A, i, ls0, s0);
         Hit h;
         h.found = true;
         h.t = hr.t;
@@ -423,7 +447,9 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
         h.node = hr.node;
         h.k = hr.k;
         Comps c;
+        RR_STAMPX(st0, 5);
         prepare(S, r, h, c);  // intersection.rs:50-60
+        RR_STAMPX(st0, 0);
         mat = S.nodes[hr.node].material;
         const DevMaterial m = S.mats[mat];
         if (S.has_transparent && needs_n1n2(m, A.rem)) {
@@ -431,6 +457,7 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
             c.n2 = A.n12[2 * i + 1];
         }
         pcol = pattern_at<CP>(S, m.pattern, world_to_object(S, hr.node, c.over), hr.node);  // material.rs:77-80
+        RR_STAMPX(st0, 1);
         if (PRE) {
             double* pl = prelit_lds(S, LC);
             for (int li = 0; li < S.n_lights; ++li) {
@@ -462,12 +489,12 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
         refl = m.reflective;
         transp = m.transparency;
         R = (m.reflective > 0.0 && m.transparency > 0.0) ? schlick(c) : 0.0;
-        event_key(A, i, ls0, sample, path);
+        event_key(A, i, ls0, s0, sample, path);
     }
     RR_STAMP(cnt, 1);
     // children of this level -> next level queue; parents -> this level's pending list
     const bool pending = do_refl || do_refr;
-    {
+    if (A.next) {  // null when no material is reflective or transparent (or at the last level)
         unsigned int* const ctr[3] = {A.lcount + LC_CHILDREN, A.lcount + LC_CHILDREN, A.lcount + LC_PENDING};
         const bool wq[3] = {do_refl, do_refr, pending};
         int32_t slots[3];
@@ -506,6 +533,9 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
     RR_STAMP(cnt, 5);
     // surface = 0 + L0 + L1 + ... (scene.rs:159-166)
     V3 surface = mk(0, 0, 0);
+#ifdef RR_STAMPS
+    if (st0) cnt.st = st0;
+#endif
     if constexpr (PRE) {
         const double* pl = prelit_lds(S, LC);
         for (int li = 0; li < S.n_lights; ++li) {
@@ -524,6 +554,9 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
         for (int li = 0; li < S.n_lights; ++li)
             light_step<G, LC>(S, A, li, has_hit, mat, over, sample, path, stash, surface, cnt);
     }
+#ifdef RR_STAMPS
+    cnt.st = st1;
+#endif
     RR_STAMP(cnt, 6);
     if (pending) {
         CombRec cr;

@@ -93,6 +93,7 @@ struct DevCamera {
     int64_t hsize, vsize;
     double half_width, half_height, pixel_size;
     double inv[16];  // full 4x4 inverse of the camera transform (camera.rs:85)
+    double origin[4];  // inverse * point(0, 0, 0), the same for every pixel (computed on the host)
 };
 
 // Conservative bounding sphere of a node's content in WORLD space (so any run of consecutive nodes,

@@ -1,0 +1,37 @@
+"""Summarise an RR_STAMPS dump (rray_amd/_exp/stamps, $RRAY_STAMPS) of the fused level-0 shade kernel:
+mean s_memtime cycles per wave between phase marks.  Region 1 = shade kernel marks, region 0 =
+the shadow walk and extra marks (render.hip, RR_STAMPX)."""
+import sys
+
+import numpy as np
+
+
+def main(path):
+    a = np.fromfile(path, dtype=np.uint64).reshape(2, 1 << 16, 8).astype(np.int64)
+    r0, r1 = a[0], a[1]
+    ok = (r1[:, 0] > 0) & (r1[:, 7] > 0)
+    r0, r1 = r0[ok], r1[ok]
+    hit = r0[:, 0] > 0  # waves with at least one hit (prepare ran)
+    rows = [("camera ray + trace prelude", r1[:, 2] - r1[:, 0], ok[ok]),
+            ("trace bundle", r1[:, 3] - r1[:, 2], ok[ok]),
+            ("trace walk", r1[:, 4] - r1[:, 3], ok[ok]),
+            ("-> prepare", r0[:, 5] - r1[:, 4], hit),
+            ("prepare", r0[:, 0] - r0[:, 5], hit),
+            ("pattern", r0[:, 1] - r0[:, 0], hit),
+            ("prelit + schlick/children", r1[:, 1] - r0[:, 1], hit),
+            ("queue appends", r1[:, 5] - r1[:, 1], ok[ok]),
+            ("shadow prelude", r0[:, 2] - r1[:, 5], hit),
+            ("shadow bundle", r0[:, 3] - r0[:, 2], hit),
+            ("shadow walk", r0[:, 4] - r0[:, 3], hit),
+            ("light final", r1[:, 6] - r0[:, 4], hit),
+            ("deliver + flush", r1[:, 7] - r1[:, 6], ok[ok]),
+            ("total", r1[:, 7] - r1[:, 0], ok[ok])]
+    print(f"waves: {ok.sum()}  with hits: {hit.sum()}")
+    for name, d, m in rows:
+        d = d[m]
+        d = d[(d >= 0) & (d < 1e8)]
+        print(f"{name:28s} mean {d.mean():9.0f}  median {np.median(d):9.0f}  (n={d.size})")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
