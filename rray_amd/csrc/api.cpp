@@ -206,7 +206,7 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             // experiment builds: per-wave phase timers of level 0 of the first batch -> $RRAY_STAMPS
             const char* stamp_path = std::getenv("RRAY_STAMPS");
             static DBuf stamp_buf;
-            const size_t stamp_bytes = (size_t)2 * (1 << 16) * 8 * sizeof(unsigned long long);
+            const size_t stamp_bytes = (size_t)2 * (1 << 16) * 16 * sizeof(unsigned long long);
             A.stamps = nullptr;
             if (stamp_path && d == 0 && base == 0) {
                 HIPCHK(stamp_buf.ensure(stamp_bytes));

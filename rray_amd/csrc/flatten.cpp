@@ -312,6 +312,25 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
         if (p.kind == RR_PAT_GRADIENT || p.kind == RR_PAT_BLEND || p.kind >= RR_PAT_PERTURBED) out.complex_patterns = 1;
         out.pats.push_back(p);
     }
+    // inline Solid leaves: a material whose root is Solid, a select pattern's Solid children
+    for (DevPattern& p : out.pats) {
+        if (p.kind != RR_PAT_STRIPE && p.kind != RR_PAT_RING && p.kind != RR_PAT_CHECKER) continue;
+        if (out.pats[p.a].kind == RR_PAT_SOLID) {
+            p.flags |= PF_A_SOLID;
+            for (int c = 0; c < 3; ++c) p.ca[c] = out.pats[p.a].color[c];
+        }
+        if (out.pats[p.b].kind == RR_PAT_SOLID) {
+            p.flags |= PF_B_SOLID;
+            for (int c = 0; c < 3; ++c) p.cb[c] = out.pats[p.b].color[c];
+        }
+    }
+    for (DevMaterial& m : out.mats) {
+        const bool white = m.pattern < 0;  // Material::default: solid white (material.rs:49)
+        if (white || out.pats[m.pattern].kind == RR_PAT_SOLID) {
+            m.root = 1;
+            for (int c = 0; c < 3; ++c) m.color[c] = white ? 1.0 : out.pats[m.pattern].color[c];
+        }
+    }
     // pattern nesting depth (the kernel evaluates trees with a bounded explicit stack)
     std::function<int(int, int)> pdepth = [&](int i, int lvl) -> int {
         if (lvl > RR_MAX_PATTERN_DEPTH) return lvl;

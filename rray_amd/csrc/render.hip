@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(256) trace_kernel(DevScene S, LevelArgs A) {
     cnt.st = nullptr;
     if (A.stamps && A.level == 0) {
         const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-        cnt.st = A.stamps + (0 * (int64_t)(1 << 16) + w) * 8;
+        cnt.st = A.stamps + (0 * (int64_t)(1 << 16) + w) * 16;
         if (w >= (1 << 16)) cnt.st = nullptr;
     }
     RR_STAMP(cnt, 0);
@@ -393,11 +393,11 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
     cnt.st = nullptr;
     if (A.stamps && A.level == 0) {
         const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-        cnt.st = w < (1 << 16) ? A.stamps + ((int64_t)(1 << 16) + w) * 8 : nullptr;
+        cnt.st = w < (1 << 16) ? A.stamps + ((int64_t)(1 << 16) + w) * 16 : nullptr;
     }
     // FUSED: the (unused) trace region of the stamp buffer takes the shadow walk and extra marks
     unsigned long long* const st1 = cnt.st;
-    unsigned long long* const st0 = (FUSED && cnt.st) ? cnt.st - (int64_t)(1 << 16) * 8 : nullptr;
+    unsigned long long* const st0 = (FUSED && cnt.st) ? cnt.st - (int64_t)(1 << 16) * 16 : nullptr;
     RR_STAMP(cnt, 0);
 #else
     unsigned long long* const st0 = nullptr;
@@ -456,7 +456,7 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
             c.n1 = A.n12[2 * i];
             c.n2 = A.n12[2 * i + 1];
         }
-        pcol = pattern_at<CP>(S, m.pattern, world_to_object(S, hr.node, c.over), hr.node);  // material.rs:77-80
+        pcol = material_color<CP>(S, m, hr.node, c.over);  // material.rs:77-80
         RR_STAMPX(st0, 1);
         if (PRE) {
             double* pl = prelit_lds(S, LC);

@@ -63,13 +63,21 @@ struct alignas(16) DevTri {
 struct alignas(16) DevMaterial {  // material.rs:35-44
     double ambient, diffuse, specular, shininess, reflective, transparency, refractive_index;
     int32_t pattern;
-    int32_t pad;
+    // root: 1 = Solid (or the default white), colour in `color` (a Solid's colour does not depend
+    // on the point, pattern.rs:151-153); 0 = evaluate pattern_at.  (Inlining a Stripe / Ring /
+    // Checker root as well made the record 224 B and cost the fused kernel 34 more spilled VGPRs.)
+    int32_t root;
+    double color[3];
 };
 
+// DevPattern.flags: NF_IDENT (identity transform) plus, for Stripe / Ring / Checker, whether child
+// a / b is a Solid whose colour is stored inline (ca / cb), saving the dependent child load.
+enum PatternFlags : int32_t { PF_A_SOLID = 2, PF_B_SOLID = 4 };
 struct alignas(16) DevPattern {  // pattern.rs:23-27
     double inv[12];
     double color[3];
     double scale;
+    double ca[3], cb[3];  // inline Solid children (PF_A_SOLID / PF_B_SOLID)
     int32_t kind, a, b, flags;
     double persistence;  // Perturbed / Noise (pattern.rs:16-19)
     int32_t octaves, pad;

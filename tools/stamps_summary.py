@@ -7,7 +7,7 @@ import numpy as np
 
 
 def main(path):
-    a = np.fromfile(path, dtype=np.uint64).reshape(2, 1 << 16, 8).astype(np.int64)
+    a = np.fromfile(path, dtype=np.uint64).reshape(2, 1 << 16, 16).astype(np.int64)
     r0, r1 = a[0], a[1]
     ok = (r1[:, 0] > 0) & (r1[:, 7] > 0)
     r0, r1 = r0[ok], r1[ok]
@@ -31,6 +31,10 @@ def main(path):
         d = d[m]
         d = d[(d >= 0) & (d < 1e8)]
         print(f"{name:28s} mean {d.mean():9.0f}  median {np.median(d):9.0f}  (n={d.size})")
+    for name, r in (("trace walk", r1), ("shadow walk", r0)):
+        w = np.maximum(r[:, 11], 1)
+        print(f"{name}: per walk  bundle-candidate chunks {np.mean(r[:, 8] / w):.2f}  "
+              f"line-passing chunks {np.mean(r[:, 9] / w):.2f}  candidate nodes {np.mean(r[:, 10] / w):.2f}")
 
 
 if __name__ == "__main__":
