@@ -174,7 +174,10 @@ def main():
     pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
+            per_kernel = json.load(open(pmc))
+            # the fused trace+shade launch is the shade_kernel<..., FUSED> instantiation in rocprof's naming
+            entry = per_kernel.get(dom) or (per_kernel.get("shade") if dom == "trace_shade" else None) or {}
+            traffic = entry.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     # SURVEY §8(d) full-scan model for the same rays: what the reference's algorithm would execute
