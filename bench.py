@@ -2,10 +2,15 @@
 
 Workload (configs[1]): synthetic 1024-sphere grid + checker plane, point light, 1920x1080, AA=1
 (scenes/c2_s1024.yaml).  One step = one frame rendered to the AA-averaged f64 image in HBM
-(Camera::render + canvas.rs box average, before `as u8`).  With N ranks (torchrun, one process per
-GPU, RCCL) the frame's rows are split in interleaved 8-row blocks and the tiles (f32) are gathered
-to rank 0 with one RCCL gather per step, double-buffered so the gather of frame k overlaps the
-render of frame k+1 ("scaling": "strong": the frame is fixed).
+(Camera::render + canvas.rs box average, before `as u8`).
+
+With N ranks (torchrun, one process per GPU) there are two shardings:
+* --mode frames (default): the job renders a batch of N frames per step, one whole C2 frame per
+  rank, each kept resident on its rank (a renderer farm's frame sharding).  No data-path collective;
+  the process group only carries the barrier and the max-over-ranks timing ("scaling": "weak").
+* --mode tiles: one frame per step, its rows split in interleaved 8-row blocks; the tiles (f32) are
+  gathered to rank 0 with one RCCL gather per step, double-buffered so the gather of frame k overlaps
+  the render of frame k+1 ("scaling": "strong": the frame is fixed).  North_star's C3 layout.
 
 Also reported: the dominant kernel's roofline (HIP events on the render stream over the timed
 region), and the CPU oracle (test-infrastructure restatement of the reference) timed on a bounded
@@ -49,6 +54,8 @@ def main():
     ap.add_argument("--workload", default="c2_s1024", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-stride", type=int, default=1, help="CPU sample: one 8-row band in every STRIDE bands")
+    ap.add_argument("--mode", choices=("frames", "tiles"), default="frames",
+                    help="multi-rank sharding: whole frames per rank (weak) or row tiles of one frame + RCCL gather")
     ap.add_argument("--force-dist", action="store_true",
                     help="rehearsal: run the multi-rank path (RCCL process group, pipelined gather) even at 1 rank")
     args = ap.parse_args()
@@ -61,9 +68,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    multi = world > 1 or args.force_dist
-    if multi:
+    distributed = world > 1 or args.force_dist
+    if distributed:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    tiles = args.mode == "tiles"
+    multi = distributed and tiles  # row tiles + pipelined gather; frames mode renders like one GPU
 
     import rray_amd as R
 
@@ -75,13 +84,14 @@ def main():
     rend.upload(scene)
     cam = scene.camera
     block = 8
-    rows = R.part_rows(H, rank, world, block)
+    part, nparts = (rank, world) if tiles else (0, 1)
+    rows = R.part_rows(H, part, nparts, block)
     dev = torch.device("cuda", local)
     from rray_amd import dist as rdist
     if not multi:
         # the AA-averaged f64 image (the drop-in's Canvas, before `as u8`)
         tile = torch.zeros((len(rows), W, 3), dtype=torch.float64, device=dev)
-        opts = R._lib.RenderOpts(aa, depth, 0, 0, rank, world, block, R._lib.RR_OUT_AVG)
+        opts = R._lib.RenderOpts(aa, depth, 0, 0, part, nparts, block, R._lib.RR_OUT_AVG)
 
         side = torch.cuda.Stream(dev) if os.environ.get("RRAY_BENCH_SIDE_STREAM") else None
 
@@ -123,7 +133,7 @@ def main():
         if multi:
             pipe.drain()
         torch.cuda.synchronize(dev)
-        if multi:
+        if distributed:
             dist.barrier()
 
     for _ in range(args.warmup):
@@ -150,7 +160,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     samples_per_frame = W * H * aa * aa
-    value = samples_per_frame * args.steps / elapsed / 1e6
+    frames_per_step = world if not tiles else 1  # frames mode: every rank renders a whole frame per step
+    value = frames_per_step * samples_per_frame * args.steps / elapsed / 1e6
 
     # roofline of the dominant kernel (rank 0's measurements)
     dom = max(ktimes, key=lambda k: ktimes[k][0])
@@ -234,19 +245,22 @@ def main():
     if rank == 0:
         line = {"metric": METRIC, "value": round(value, 3), "unit": "Mpixel-samples/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+                "higher_is_better": True,
+                "scaling": "strong" if tiles else "weak", "vs_baseline": None, "dtype": "f64",
                 "data": "synthetic (scenes/make_scenes.py, seeded)",
                 "config": {"workload": args.workload, "scene": scene_file, "width": W, "height": H, "aa": aa,
                            "max_depth": depth, "samples_per_step": samples_per_frame, "objects": counts["objects"],
-                           "parallelism": f"row-tiles x{world}" + (" + pipelined rccl gather (f32 tiles)"
-                                                                 if world > 1 else "")},
+                           "frames_per_step": frames_per_step,
+                           "parallelism": (f"row-tiles x{world}" + (" + pipelined rccl gather (f32 tiles)"
+                                                                    if world > 1 else "")) if tiles else
+                           f"frame-parallel x{world} (one whole frame per rank per step, no data-path collective)"},
                 "roofline": roofline, "cpu_baseline": cpu, "parity_sample": parity,
                 "kernels_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in ktimes.items() if v[1]},
                 "host_enqueue_ms_per_step": round((t_enq - t0) / args.steps * 1e3, 4),
                 "stats_last_step": {k: stats[k] for k in ("rays", "shadow_rays", "shade_events", "n1n2_scans",
                                                           "prim_tests", "exact_flops", "wave_visits")}}
         print(json.dumps(line), flush=True)
-    if multi:
+    if distributed:
         dist.barrier()
         dist.destroy_process_group()
     rend.close()
