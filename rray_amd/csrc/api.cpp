@@ -184,6 +184,12 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
                 HIPCHK(hipMemsetAsync(c->lcount.p, 0, rr::LC_COUNT * sizeof(unsigned int), st));
             rr::LevelArgs A = base_args;
             A.base = base;
+            // level-0 index math: magic divisors, and the wave-uniform tile path when every tile is
+            // a full 8x8 and this batch starts on a tile boundary
+            A.aa_magic = A.aa > 1 ? (uint32_t)((1ull << 32) / (uint64_t)A.aa) : 0u;
+            A.br_magic = A.block_rows > 1 ? (uint32_t)((1ull << 32) / (uint64_t)A.block_rows) : 0u;
+            A.tile_fast = !A.rays0 && A.lrows > 0 && A.hs % 8 == 0 && A.lrows % 8 == 0 && base % 64 == 0 ? 1 : 0;
+            A.tiles_per_row = (uint32_t)(A.hs / 8);
             A.level = d;
             A.rem = max_depth - d;
             A.n = n;
@@ -515,6 +521,8 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     HIPCHK(hipEventRecord(c->e0, st));
     rr::LevelArgs A{};
     A.cam = dev_camera(cam);
+    A.cam_affine = A.cam.inv[12] == 0.0 && A.cam.inv[13] == 0.0 && A.cam.inv[14] == 0.0 && A.cam.inv[15] == 1.0 &&
+                   A.cam.origin[3] == 1.0;
     A.hs = cam->hsize;
     A.lrows = local_rows;
     A.aa = o->aa;

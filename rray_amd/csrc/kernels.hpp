@@ -16,6 +16,10 @@ struct LevelArgs {
     int64_t hs;              // supersampled width
     int64_t lrows;           // part-local supersampled rows (level-0 camera rays run in 8x8 tiles)
     int32_t aa, part, nparts, block_rows;
+    uint32_t aa_magic, br_magic;  // floor(2^32 / d) for d = aa, block_rows (>= 2; 0 when d == 1)
+    int32_t tile_fast;       // level-0 tiles all full 8x8 and the batch tile-aligned: wave = one tile
+    uint32_t tiles_per_row;  // hs / 8 (tile_fast)
+    int32_t cam_affine;      // camera inverse row 3 == (0, 0, 0, 1)
     int64_t base;            // first local sample of this batch
     const double* rays0;     // level-0 explicit rays (o xyz, d xyz); nullptr: camera rays
     int32_t level, rem;      // level d and `remaining` = max_depth - d

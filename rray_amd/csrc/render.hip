@@ -18,26 +18,83 @@
 
 namespace rr {
 
-// local sample index of this part -> (px, py) on the supersampled canvas (interleaved row blocks).
-// 32-bit arithmetic: rr_render_device rejects parts of 2^31 samples or more.
-__device__ __forceinline__ void local_to_pixel(const LevelArgs& A, uint32_t ls, uint32_t& px, uint32_t& py) {
-    const uint32_t hs = (uint32_t)A.hs, aa = (uint32_t)A.aa, br = (uint32_t)A.block_rows;
-    const uint32_t lrow = ls / hs;
-    px = ls - lrow * hs;
-    const uint32_t k = lrow / aa, sub = lrow - k * aa;
-    const uint32_t bi = k / br, kb = k - bi * br;
-    const uint32_t y = (bi * (uint32_t)A.nparts + (uint32_t)A.part) * br + kb;
-    py = y * aa + sub;
+// floor(n / d) for d >= 1 given magic = floor(2^32 / d) (d >= 2; unused for d == 1): the high
+// product is the quotient or one less for every 32-bit n, so one correction makes it exact.
+__device__ __forceinline__ uint32_t magic_div(uint32_t n, uint32_t d, uint32_t magic) {
+    if (d == 1u) return n;
+    uint32_t q = __umulhi(n, magic);
+    if (n - q * d >= d) ++q;
+    return q;
 }
 
-// Camera::ray_for_pixel (camera.rs:75-93) with the full 4x4 camera inverse (w included)
-__device__ __forceinline__ Ray camera_ray(const DevCamera& C, uint32_t px, uint32_t py) {
+// A level-0 event's canvas position: ls = part-local row-major sample index (the output index),
+// (px, py) = supersampled canvas pixel.  Camera events run in tile order (tile_to_local); when every
+// tile is a full 8x8 and the batch is tile-aligned (A.tile_fast, host-checked) a wave is exactly one
+// tile, so the tile arithmetic is wave-uniform (scalar) and a lane only adds its (lane & 7, lane >> 3)
+// offset — the same bijection as tile_to_local_u32 without its three per-lane divisions.
+struct Px0 {
+    uint32_t ls, px, py;
+};
+// OWN: i is this thread's own index (blockIdx.x * 256 + threadIdx.x), so the wave's tile is uniform;
+// otherwise (events from a list) the same mapping is computed per lane from i.
+template <bool OWN>
+__device__ __forceinline__ Px0 level0_px(const LevelArgs& A, int64_t i) {
+    Px0 r;
+    if (A.rays0) {
+        r.ls = (uint32_t)(A.base + i);
+        r.px = r.py = 0u;
+        return r;
+    }
+    const uint32_t hs = (uint32_t)A.hs;
+    uint32_t lrow;
+    if (A.tile_fast) {
+        const uint32_t t = (uint32_t)(A.base + i);
+        const uint32_t T = OWN ? (uint32_t)(A.base >> 6) + blockIdx.x * 4u + (uint32_t)uniform((int)(threadIdx.x >> 6))
+                               : t >> 6;
+        const uint32_t band = T / A.tiles_per_row;
+        const uint32_t tc = T - band * A.tiles_per_row;
+        const uint32_t lane = OWN ? threadIdx.x & 63u : t & 63u;
+        lrow = band * 8u + (lane >> 3);
+        r.px = tc * 8u + (lane & 7u);
+        r.ls = lrow * hs + r.px;
+    } else {
+        const uint32_t t = (uint32_t)(A.base + i);
+        r.ls = A.lrows <= 0 ? t : tile_to_local_u32(t, hs, (uint32_t)A.lrows);
+        lrow = r.ls / hs;
+        r.px = r.ls - lrow * hs;
+    }
+    // interleaved row blocks of the part -> canvas row (32-bit: rr_render_device rejects parts of
+    // 2^31 samples or more)
+    const uint32_t aa = (uint32_t)A.aa, br = (uint32_t)A.block_rows;
+    const uint32_t k = magic_div(lrow, aa, A.aa_magic), sub = lrow - k * aa;
+    const uint32_t bi = magic_div(k, br, A.br_magic), kb = k - bi * br;
+    const uint32_t y = (bi * (uint32_t)A.nparts + (uint32_t)A.part) * br + kb;
+    r.py = y * aa + sub;
+    return r;
+}
+template <bool OWN>
+__device__ __forceinline__ Px0 level0_px_if(const LevelArgs& A, int64_t i) {
+    if (A.level > 0) return {0u, 0u, 0u};
+    return level0_px<OWN>(A, i);
+}
+
+// Camera::ray_for_pixel (camera.rs:75-93).  The camera inverse's 4th row is (0, 0, 0, 1) for every
+// view_transform (checked on the host, A.cam_affine), so pixel.w == 1 == origin.w and the w terms of
+// the subtraction and of the magnitude are exactly +0 (adding +0 to a sum of squares is exact).
+__device__ __forceinline__ Ray camera_ray(const DevCamera& C, bool affine, uint32_t px, uint32_t py) {
     double xoffset = ((double)px + 0.5) * C.pixel_size;
     double yoffset = ((double)py + 0.5) * C.pixel_size;
     double wx = C.half_width - xoffset;
     double wy = C.half_height - yoffset;
     const double* M = C.inv;
     const double* ow = C.origin;  // M * point(0, 0, 0): pixel-independent, computed on the host
+    if (affine) {
+        double pw[3];
+        for (int r = 0; r < 3; ++r) pw[r] = M[4 * r] * wx + M[4 * r + 1] * wy + M[4 * r + 2] * -1.0 + M[4 * r + 3] * 1.0;
+        double dx = pw[0] - ow[0], dy = pw[1] - ow[1], dz = pw[2] - ow[2];
+        double mag = sqrt(dx * dx + dy * dy + dz * dz);
+        return {mk(ow[0], ow[1], ow[2]), mk(dx / mag, dy / mag, dz / mag)};
+    }
     double pw[4];
     for (int r = 0; r < 4; ++r) pw[r] = M[4 * r] * wx + M[4 * r + 1] * wy + M[4 * r + 2] * -1.0 + M[4 * r + 3] * 1.0;
     double dx = pw[0] - ow[0], dy = pw[1] - ow[1], dz = pw[2] - ow[2], dw = pw[3] - ow[3];
@@ -45,15 +102,9 @@ __device__ __forceinline__ Ray camera_ray(const DevCamera& C, uint32_t px, uint3
     return {mk(ow[0], ow[1], ow[2]), mk(dx / mag, dy / mag, dz / mag)};
 }
 
-// row-major local sample index of level-0 event i (camera events run in tile order)
-__device__ __forceinline__ uint32_t level0_local(const LevelArgs& A, int64_t i) {
-    const uint32_t t = (uint32_t)(A.base + i);
-    return (A.rays0 || A.lrows <= 0) ? t : tile_to_local_u32(t, (uint32_t)A.hs, (uint32_t)A.lrows);
-}
-
-// the ray of event i at this level; ls = level0_local(A, i) (used at level 0 only); camera rays also
+// the ray of event i at this level; q = level0_px(A, i) (used at level 0 only); camera rays also
 // return their global sample id (the jitter key, as event_key) in s0
-__device__ __forceinline__ Ray event_ray(const LevelArgs& A, int64_t i, uint32_t ls, uint64_t& s0) {
+__device__ __forceinline__ Ray event_ray(const LevelArgs& A, int64_t i, const Px0& q, uint64_t& s0) {
     if (A.level > 0) {
         const Event& e = A.ev[i];
         return {mk(e.o[0], e.o[1], e.o[2]), mk(e.d[0], e.d[1], e.d[2])};
@@ -62,30 +113,36 @@ __device__ __forceinline__ Ray event_ray(const LevelArgs& A, int64_t i, uint32_t
         const double* p = A.rays0 + 6 * (A.base + i);
         return {mk(p[0], p[1], p[2]), mk(p[3], p[4], p[5])};
     }
-    uint32_t px, py;
-    local_to_pixel(A, ls, px, py);
-    s0 = (uint64_t)py * (uint64_t)A.hs + px;
-    return camera_ray(A.cam, px, py);
+    s0 = (uint64_t)q.py * (uint64_t)A.hs + q.px;
+    return camera_ray(A.cam, A.cam_affine, q.px, q.py);
 }
+template <bool OWN>
 __device__ __forceinline__ Ray event_ray(const LevelArgs& A, int64_t i) {
     uint64_t s0 = 0;
-    return event_ray(A, i, A.level > 0 ? 0u : level0_local(A, i), s0);
+    return event_ray(A, i, level0_px_if<OWN>(A, i), s0);
 }
-// jitter identity of event i: (global sample id, recursion path); ls as for event_ray
+// jitter identity of event i: (global sample id, recursion path); q as for event_ray
 // (s0: event_ray's sample id of a level-0 camera ray)
-__device__ __forceinline__ void event_key(const LevelArgs& A, int64_t i, uint32_t ls0, uint64_t s0, uint64_t& sample,
+__device__ __forceinline__ void event_key(const LevelArgs& A, int64_t i, const Px0& q, uint64_t s0, uint64_t& sample,
                                           uint32_t& path) {
-    const uint32_t ls = A.level > 0 ? A.ev[i].sample : ls0;
     path = A.level > 0 ? A.ev[i].path : 1u;
-    if (A.level == 0 && !A.rays0) {
-        sample = s0;
-    } else if (A.rays0) {
-        sample = (uint64_t)ls;
-    } else {
-        uint32_t px, py;
-        local_to_pixel(A, ls, px, py);
-        sample = (uint64_t)py * (uint64_t)A.hs + px;
+    if (A.level == 0) {
+        sample = A.rays0 ? (uint64_t)q.ls : s0;
+        return;
     }
+    const uint32_t ls = A.ev[i].sample;
+    if (A.rays0) {
+        sample = (uint64_t)ls;
+        return;
+    }
+    // level >= 1: the event carries its camera sample's local index (row-major)
+    const uint32_t hs = (uint32_t)A.hs;
+    const uint32_t lrow = ls / hs, px = ls - lrow * hs;
+    const uint32_t aa = (uint32_t)A.aa, br = (uint32_t)A.block_rows;
+    const uint32_t k = magic_div(lrow, aa, A.aa_magic), sub = lrow - k * aa;
+    const uint32_t bi = magic_div(k, br, A.br_magic), kb = k - bi * br;
+    const uint32_t y = (bi * (uint32_t)A.nparts + (uint32_t)A.part) * br + kb;
+    sample = (uint64_t)(y * aa + sub) * (uint64_t)A.hs + px;
 }
 
 // Block-aggregated queue appends: the 4 waves' ballots are summed in LDS and one lane per queue
@@ -163,7 +220,7 @@ __global__ void __launch_bounds__(256) trace_kernel(DevScene S, LevelArgs A) {
     }
     RR_STAMP(cnt, 0);
 #endif
-    Ray r = valid ? event_ray(A, i) : Ray{mk(0, 0, 0), mk(0, 0, 1)};
+    Ray r = valid ? event_ray<true>(A, i) : Ray{mk(0, 0, 0), mk(0, 0, 1)};
     Hit h;
     RR_STAMP(cnt, 1);
     trace_closest<G, LC>(S, r, valid, h, cnt);
@@ -207,7 +264,7 @@ __global__ void __launch_bounds__(256) n1n2_kernel(DevScene S, LevelArgs A) {
     const bool valid = j < cnt_n;
     Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int64_t i = valid ? A.n1n2_list[j] : 0;
-    Ray r = valid ? event_ray(A, i) : Ray{mk(0, 0, 0), mk(0, 0, 1)};
+    Ray r = valid ? event_ray<false>(A, i) : Ray{mk(0, 0, 0), mk(0, 0, 1)};
     Hit h;
     h.found = valid;
     h.t = 0.0;
@@ -402,13 +459,14 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
 #else
     unsigned long long* const st0 = nullptr;
 #endif
-    const uint32_t ls0 = A.level > 0 ? 0u : level0_local(A, i);
+    const Px0 q0 = level0_px_if<true>(A, i);
+    const uint32_t ls0 = q0.ls;
     HitRec hr;
     hr.node = -1;
     Ray r0 = {mk(0, 0, 0), mk(0, 0, 1)};  // FUSED: the event's ray, traced here
     uint64_t s0 = 0;  // level-0 sample id from event_ray
     if (FUSED) {
-        if (valid) r0 = event_ray(A, i, ls0, s0);
+        if (valid) r0 = event_ray(A, i, q0, s0);
         Hit th;
         trace_closest<G, LC>(S, r0, valid, th, cnt);
         cnt.rays += popc_ballot(valid);
@@ -438,7 +496,7 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
     uint64_t sample = 0;
     uint32_t path = 1u;
     if (has_hit) {
-        const Ray r = FUSED ? r0 : event_ray(A, i, ls0, s0);
+        const Ray r = FUSED ? r0 : event_ray(A, i, q0, s0);
         Hit h;
         h.found = true;
         h.t = hr.t;
@@ -489,7 +547,7 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
         refl = m.reflective;
         transp = m.transparency;
         R = (m.reflective > 0.0 && m.transparency > 0.0) ? schlick(c) : 0.0;
-        event_key(A, i, ls0, s0, sample, path);
+        event_key(A, i, q0, s0, sample, path);
     }
     RR_STAMP(cnt, 1);
     // children of this level -> next level queue; parents -> this level's pending list
