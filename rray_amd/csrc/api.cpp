@@ -80,7 +80,10 @@ struct rr_ctx {
     hipStream_t last_st = nullptr;  // stream of the last render (the context's workspace is ordered on it)
     rr_stats last{};
     bool stats_pending = false;
-    int64_t batch = (int64_t)1 << 23;
+    // camera samples per wavefront pass: large, so that the deep levels of a frame (few, slow,
+    // incoherent rays) run once per frame rather than once per batch; the queues of a 2^27-sample
+    // pass need ~50 GB at depth 5, well inside the 288 GB of HBM
+    int64_t batch = (int64_t)1 << 27;
     // per-kernel timing (rr_kernel_times)
     bool profile = false;
     rr::KernelProf prof;

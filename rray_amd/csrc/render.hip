@@ -204,7 +204,7 @@ __device__ __forceinline__ void zero_next_counters(const LevelArgs& A) {
         A.counters_zero[j] = 0ull;
 }
 
-template <int G, bool LC>
+template <int G, bool LC, bool RM>
 __global__ void __launch_bounds__(256) trace_kernel(DevScene S, LevelArgs A) {
     zero_next_counters(A);
     if (LC) stage_culls(S);
@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(256) trace_kernel(DevScene S, LevelArgs A) {
     Ray r = valid ? event_ray<true>(A, i) : Ray{mk(0, 0, 0), mk(0, 0, 1)};
     Hit h;
     RR_STAMP(cnt, 1);
-    trace_closest<G, LC>(S, r, valid, h, cnt);
+    trace_closest<G, LC, RM>(S, r, valid, h, cnt);
     cnt.rays += popc_ballot(valid);
     if (valid) {
         HitRec hr;
@@ -256,7 +256,7 @@ __global__ void __launch_bounds__(256) trace_kernel(DevScene S, LevelArgs A) {
 #endif
 }
 
-template <int G, bool LC>
+template <int G, bool LC, bool RM>
 __global__ void __launch_bounds__(256) n1n2_kernel(DevScene S, LevelArgs A) {
     if (LC) stage_culls(S);
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -281,7 +281,7 @@ __global__ void __launch_bounds__(256) n1n2_kernel(DevScene S, LevelArgs A) {
         h.rank = S.nodes[hr.node].rank;
     }
     double n1 = 1.0, n2 = 1.0;
-    n1n2_walk<G, LC>(S, r, h, valid, n1, n2, cnt);
+    n1n2_walk<G, LC, RM>(S, r, h, valid, n1, n2, cnt);
     if (valid) {
         A.n12[2 * i] = n1;
         A.n12[2 * i + 1] = n2;
@@ -341,11 +341,11 @@ __device__ __forceinline__ void deliver(int32_t level, int64_t i, int32_t parent
 
 // intensity_at (light.rs:67-96): 1 - in_shadow from is_shadowed toward the light (point) or the
 // fraction of its level^2 jittered cell samples that are shadowed (area, light.rs:47-65)
-template <int G, bool LC>
+template <int G, bool LC, bool RM>
 __device__ __forceinline__ double shadow_amount(const DevScene& S, const LevelArgs& A, const DevLight& Lt, int li,
                                                 V3 over, bool active, uint64_t sample, uint32_t path, Counters& cnt) {
     if (Lt.kind == RR_LIGHT_POINT)
-        return shadowed<G, LC>(S, over, mk(Lt.position[0], Lt.position[1], Lt.position[2]), active, cnt) ? 1.0 : 0.0;
+        return shadowed<G, LC, RM>(S, over, mk(Lt.position[0], Lt.position[1], Lt.position[2]), active, cnt) ? 1.0 : 0.0;
     const int amount = Lt.level * Lt.level;
     int total = 0;
     for (int s = 0; s < amount; ++s) {
@@ -359,7 +359,7 @@ __device__ __forceinline__ double shadow_amount(const DevScene& S, const LevelAr
         const double vf = ((double)row + vr) / (double)Lt.level;
         const V3 target = vadd(vadd(mk(Lt.corner[0], Lt.corner[1], Lt.corner[2]), vmul(mk(Lt.u[0], Lt.u[1], Lt.u[2]), uf)),
                                vmul(mk(Lt.v[0], Lt.v[1], Lt.v[2]), vf));
-        total += shadowed<G, LC>(S, over, target, active, cnt) ? 1 : 0;
+        total += shadowed<G, LC, RM>(S, over, target, active, cnt) ? 1 : 0;
     }
     return (double)total / (double)amount;
 }
@@ -393,12 +393,12 @@ __device__ __forceinline__ void stash_put(ShadeStash& s, V3 eyev, V3 normalv, V3
 
 // one light of shade_hit's sum: surface += lighting(material, light, colour, over, eyev, normalv,
 // intensity_at(light, over)) — the shadow walk first, then the lighting terms from the stash
-template <int G, bool LC>
+template <int G, bool LC, bool RM>
 __device__ __forceinline__ void light_step(const DevScene& S, const LevelArgs& A, int li, bool has_hit, int mat,
                                            V3 over, uint64_t sample, uint32_t path, const ShadeStash& st,
                                            V3& surface, Counters& cnt) {
     const DevLight Lt = ldc(S.lights, li);
-    const double in_shadow = shadow_amount<G, LC>(S, A, Lt, li, over, has_hit, sample, path, cnt);
+    const double in_shadow = shadow_amount<G, LC, RM>(S, A, Lt, li, over, has_hit, sample, path, cnt);
     if (has_hit) {
         const int t = threadIdx.x;
         const V3 eyev = mk(st.v[0][t], st.v[1][t], st.v[2][t]);
@@ -438,14 +438,27 @@ __device__ __forceinline__ void light_step(const DevScene& S, const LevelArgs& A
 // CP: the scene has Gradient / Blend / Perturbed / Noise / Texture patterns, evaluated by the
 // out-of-line pattern_tree.  Without CP the kernel carries no call at all: the call graph's register
 // demand (atan2 / acos / Perlin in the callee) otherwise costs the common scenes their occupancy.
-template <int G, bool LC, bool FUSED, bool PRE, bool CP>
+template <int G, bool LC, bool FUSED, bool PRE, bool CP, bool RM>
 __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevScene S, LevelArgs A) {
+#ifdef RR_STAMPS
+    // kernel entry (before the counter clear and the cull staging) and the wave's hardware slot
+    if (A.stamps && A.level == 0 && (threadIdx.x & 63) == 0) {
+        const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        if (w < (1 << 16)) {
+            unsigned long long* e = A.stamps + ((int64_t)(1 << 16) + w) * 16;
+            e[12] = __builtin_amdgcn_s_memtime();
+            e[13] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+            e[14] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+        }
+    }
+#endif
     zero_next_counters(A);
     if (LC) stage_culls(S);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < A.n;
     Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t trace_flops = 0, trace_visits = 0;
+    uint64_t trace_flops = 0;
+    uint32_t trace_visits = 0;
 #ifdef RR_STAMPS
     cnt.st = nullptr;
     if (A.stamps && A.level == 0) {
@@ -468,7 +481,7 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
     if (FUSED) {
         if (valid) r0 = event_ray(A, i, q0, s0);
         Hit th;
-        trace_closest<G, LC>(S, r0, valid, th, cnt);
+        trace_closest<G, LC, RM>(S, r0, valid, th, cnt);
         cnt.rays += popc_ballot(valid);
         hr.t = th.t;
         hr.u = th.u;
@@ -598,7 +611,7 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
         const double* pl = prelit_lds(S, LC);
         for (int li = 0; li < S.n_lights; ++li) {
             const DevLight Lt = ldc(S.lights, li);
-            const double in_shadow = shadow_amount<G, LC>(S, A, Lt, li, over, has_hit, sample, path, cnt);
+            const double in_shadow = shadow_amount<G, LC, RM>(S, A, Lt, li, over, has_hit, sample, path, cnt);
             if (has_hit) {
                 const int t = threadIdx.x;
                 const double* q = pl + li * 6 * 256 + t;
@@ -610,7 +623,7 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
         __shared__ ShadeStash stash;
         stash_put(stash, eyev, normalv, pcol);
         for (int li = 0; li < S.n_lights; ++li)
-            light_step<G, LC>(S, A, li, has_hit, mat, over, sample, path, stash, surface, cnt);
+            light_step<G, LC, RM>(S, A, li, has_hit, mat, over, sample, path, stash, surface, cnt);
     }
 #ifdef RR_STAMPS
     cnt.st = st1;
@@ -692,7 +705,7 @@ __global__ void __launch_bounds__(256) shadow_query_kernel(DevScene S, const dou
         p = mk(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]);
         l = mk(lps[3 * i], lps[3 * i + 1], lps[3 * i + 2]);
     }
-    bool sh = shadowed<G, LC>(S, p, l, valid, cnt);
+    bool sh = shadowed<G, LC, true>(S, p, l, valid, cnt);
     if (valid) out[i] = sh ? 1 : 0;
     flush(cnt, counters, W_SHADOW);
 }
@@ -734,20 +747,37 @@ struct Span {  // brackets one launch with events when profiling
 };
 }  // namespace
 
-template <int G, bool LC, bool FUSED>
-static void launch_shade(const DevScene& S, const LevelArgs& A, hipStream_t st, bool pre, size_t lds) {
+template <int G, bool LC, bool FUSED, bool RM>
+static void launch_shade_rm(const DevScene& S, const LevelArgs& A, hipStream_t st, bool pre, size_t lds) {
     const dim3 grid(blocks_for(A.n)), block(256);
+#ifdef RR_QUICK
+    if (pre)
+        hipLaunchKernelGGL((shade_kernel<G, LC, FUSED, true, false, RM>), grid, block, lds, st, S, A);
+    else
+        hipLaunchKernelGGL((shade_kernel<G, LC, FUSED, false, false, RM>), grid, block, lds, st, S, A);
+#else
     if (S.complex_patterns) {
         if (pre)
-            hipLaunchKernelGGL((shade_kernel<G, LC, FUSED, true, true>), grid, block, lds, st, S, A);
+            hipLaunchKernelGGL((shade_kernel<G, LC, FUSED, true, true, RM>), grid, block, lds, st, S, A);
         else
-            hipLaunchKernelGGL((shade_kernel<G, LC, FUSED, false, true>), grid, block, lds, st, S, A);
+            hipLaunchKernelGGL((shade_kernel<G, LC, FUSED, false, true, RM>), grid, block, lds, st, S, A);
     } else {
         if (pre)
-            hipLaunchKernelGGL((shade_kernel<G, LC, FUSED, true, false>), grid, block, lds, st, S, A);
+            hipLaunchKernelGGL((shade_kernel<G, LC, FUSED, true, false, RM>), grid, block, lds, st, S, A);
         else
-            hipLaunchKernelGGL((shade_kernel<G, LC, FUSED, false, false>), grid, block, lds, st, S, A);
+            hipLaunchKernelGGL((shade_kernel<G, LC, FUSED, false, false, RM>), grid, block, lds, st, S, A);
     }
+#endif
+}
+// RM (ray-major chunk tests, walk_nodes) for the secondary levels, whose waves are often
+// incoherent; level 0 (camera tiles and their shadow rays) runs without it, which keeps the camera
+// kernels' registers.
+template <int G, bool LC, bool FUSED>
+static void launch_shade(const DevScene& S, const LevelArgs& A, hipStream_t st, bool pre, size_t lds) {
+    if (A.level > 0)
+        launch_shade_rm<G, LC, FUSED, true>(S, A, st, pre, lds);
+    else
+        launch_shade_rm<G, LC, FUSED, false>(S, A, st, pre, lds);
 }
 
 template <int G, bool LC>
@@ -761,11 +791,17 @@ static void launch_level_t(const DevScene& S, const LevelArgs& A, hipStream_t st
     }
     {
         Span s(prof, K_TRACE, st);
-        hipLaunchKernelGGL((trace_kernel<G, LC>), dim3(blocks_for(A.n)), dim3(256), cull_lds(S), st, S, A);
+        if (A.level > 0)
+            hipLaunchKernelGGL((trace_kernel<G, LC, true>), dim3(blocks_for(A.n)), dim3(256), cull_lds(S), st, S, A);
+        else
+            hipLaunchKernelGGL((trace_kernel<G, LC, false>), dim3(blocks_for(A.n)), dim3(256), cull_lds(S), st, S, A);
     }
     if (S.has_transparent) {
         Span s(prof, K_N1N2, st);
-        hipLaunchKernelGGL((n1n2_kernel<G, LC>), dim3(blocks_for(A.n)), dim3(256), cull_lds(S), st, S, A);
+        if (A.level > 0)
+            hipLaunchKernelGGL((n1n2_kernel<G, LC, true>), dim3(blocks_for(A.n)), dim3(256), cull_lds(S), st, S, A);
+        else
+            hipLaunchKernelGGL((n1n2_kernel<G, LC, false>), dim3(blocks_for(A.n)), dim3(256), cull_lds(S), st, S, A);
     }
     {
         Span s(prof, K_SHADE, st);
@@ -776,6 +812,10 @@ static void launch_level_t(const DevScene& S, const LevelArgs& A, hipStream_t st
 hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t st, KernelProf* prof) {
     if (A.n <= 0) return hipSuccess;
     const int g = S.general ? 2 : S.has_groups ? 1 : 0;  // G: flat / groups / general (CSG, 4-entry leaves)
+#ifdef RR_QUICK  // experiment builds: only the flat, LDS-culled, simple-pattern kernels (fast compiles)
+    if (g != 0 || !S.lds_culls || S.complex_patterns) return hipErrorNotSupported;
+    launch_level_t<0, true>(S, A, st, prof);
+#else
     if (g == 2) {
         if (S.lds_culls)
             launch_level_t<2, true>(S, A, st, prof);
@@ -792,6 +832,7 @@ hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t st, K
         else
             launch_level_t<0, false>(S, A, st, prof);
     }
+#endif
     return hipGetLastError();
 }
 

@@ -145,6 +145,7 @@ struct DevScene {
 // Node culls (16 B each) and chunk records (32 B each) are copied into LDS by every walking
 // workgroup when together they fit in this many bytes.
 constexpr int RR_LDS_CULL_BYTES = 40 * 1024;
+constexpr int RR_BUNDLE_MIN_NODES = 8;  // walks of scenes with at most this many nodes build no ray bundle
 
 // Per-launch counters (u64, zeroed by the host before each launch).
 enum Counter {

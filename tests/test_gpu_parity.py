@@ -195,6 +195,26 @@ def test_multi_part_tiles_are_bit_identical(renderer, R):
         assert np.array_equal(img, full), nparts
 
 
+def test_batched_passes_are_bit_identical(renderer, R):
+    """A frame split into many wavefront passes (RRAY_BATCH) renders the same image as one pass."""
+    scene, _ = _yaml_pair("c3_s1024_reflect.yaml", 48, 27, 2)
+    renderer.upload(scene)
+    one = renderer.render(scene.camera, aa=2, canvas=True)
+    os.environ["RRAY_BATCH"] = "1024"
+    try:
+        small = R.Renderer(0)
+    finally:
+        del os.environ["RRAY_BATCH"]
+    try:
+        small.upload(scene)
+        many = small.render(scene.camera, aa=2, canvas=True)  # 96x54 samples -> 6 passes
+    finally:
+        small.close()
+    assert np.array_equal(one["canvas"], many["canvas"])
+    assert np.array_equal(one["avg"], many["avg"])
+    assert one["stats"]["rays"] == many["stats"]["rays"]
+
+
 # ---------------------------------------------------------------- known-answer tests through the GPU
 def default_scene(R, O=None):
     """scene.rs:79-92 on both sides."""

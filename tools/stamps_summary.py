@@ -39,3 +39,34 @@ def main(path):
 
 if __name__ == "__main__":
     main(sys.argv[1])
+
+
+def occupancy(path):
+    """Kernel-entry stamps (slot 12) and hardware ids (13: HW_ID, 14: XCC_ID): time before phase 0
+    (counter clear + cull staging) and how fully each CU's 16 wave slots were kept busy."""
+    a = np.fromfile(path, dtype=np.uint64).reshape(2, 1 << 16, 16).astype(np.int64)
+    r1 = a[1]
+    ok = (r1[:, 12] > 0) & (r1[:, 7] > 0)
+    r1 = r1[ok]
+    if not len(r1):
+        return
+    ent, end, p0 = r1[:, 12], r1[:, 7], r1[:, 0]
+    print(f"entry -> phase 0 (clear + staging): mean {np.mean(p0 - ent):.0f}  median {np.median(p0 - ent):.0f}")
+    hw, xcc = r1[:, 13], r1[:, 14] & 0xf
+    cu = (xcc << 8) | (((hw >> 13) & 0x7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 0xf)
+    simd = (cu << 2) | ((hw >> 4) & 3)
+    effs, spans = [], []
+    for c in np.unique(cu):
+        m = cu == c
+        span = end[m].max() - ent[m].min()
+        spans.append(span)
+        effs.append(np.sum(end[m] - ent[m]) / (span * 16.0))
+    print(f"CUs {len(effs)}  span mean {np.mean(spans):.0f} min {np.min(spans):.0f} max {np.max(spans):.0f}  "
+          f"wave-slot occupancy mean {np.mean(effs):.3f}")
+    per_simd = np.bincount(np.searchsorted(np.unique(simd), simd))
+    print(f"waves per SIMD: mean {per_simd.mean():.1f} min {per_simd.min()} max {per_simd.max()}")
+    print(f"wave life (entry -> end): mean {np.mean(end - ent):.0f}")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1:
+    occupancy(sys.argv[1])
