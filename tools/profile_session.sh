@@ -8,7 +8,9 @@ OUT=$ROOTDIR/gpurun_out/prof
 WL=${WL:-c2_s1024}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-python -c "import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1 || exit 1
+if [ "${SKIP_BUILD:-0}" != 1 ]; then
+  python -c "import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1 || exit 1
+fi
 run() {  # name, timeout, rocprof args...
   local name=$1 t=$2; shift 2
   echo "== $name ($(date +%T))"
