@@ -131,6 +131,8 @@ typedef struct {
 #define RR_OUT_AVG 2       /* write the AA-averaged image (canvas.rs:76-96, before `as u8`) */
 #define RR_OUT_AVG_F32 4   /* rr_render_device only: the AA-averaged image rounded to float (3 floats per
                               pixel; the average itself is computed in f64) — compact tiles for gathers */
+#define RR_NO_FRAME_TIMING 8 /* rr_render_device only: no HIP event pair around the frame (each event
+                                record costs the stream a few microseconds); rr_stats.kernel_ms is 0 */
 
 typedef struct {
     uint64_t rays;          /* closest-hit rays (primary + reflected + refracted) */
@@ -140,7 +142,7 @@ typedef struct {
     uint64_t group_tests, group_hits;
     uint64_t samples;       /* pixel x AA samples rendered */
     uint64_t prim_tests;    /* exact f64 leaf tests executed (lane-level, after culling) */
-    double kernel_ms;       /* render + AA kernels, HIP events */
+    double kernel_ms;       /* render + AA kernels, HIP events (0 with RR_NO_FRAME_TIMING) */
     uint64_t exact_flops[3];  /* f64 flops of those tests (SURVEY §8d model) per walk: trace, shadow, n1n2 */
     uint64_t wave_visits[3];  /* wave-level node visits (exact test issued for a 64-lane wave), same order */
 } rr_stats;

@@ -16,6 +16,7 @@ ERRORS = {-1: "RR_E_ARG", -2: "RR_E_HIP", -3: "RR_E_SCENE", -4: "RR_E_NONAFFINE"
           -7: "RR_E_NAN"}
 globals().update({name: code for code, name in ERRORS.items()})  # RR_E_ARG = -1, ...
 RR_OUT_CANVAS, RR_OUT_AVG, RR_OUT_AVG_F32 = 1, 2, 4
+RR_NO_FRAME_TIMING = 8  # rr_render_device: no per-frame HIP event pair (rr_stats.kernel_ms = 0)
 SPHERE, PLANE, GROUP, TRIANGLE, SMOOTH_TRIANGLE, CUBE, CYLINDER, CONE, CSG, TORUS = range(10)
 CSG_OPS = {"union": 0, "intersection": 1, "difference": 2}
 PAT = {"test": 0, "solid": 1, "stripe": 2, "gradient": 3, "ring": 4, "checker": 5, "blend": 6, "perturbed": 7,

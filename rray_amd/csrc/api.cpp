@@ -80,6 +80,7 @@ struct rr_ctx {
     hipStream_t last_st = nullptr;  // stream of the last render (the context's workspace is ordered on it)
     rr_stats last{};
     bool stats_pending = false;
+    bool frame_timed = true;  // e0/e1 bracket the last frame
     // camera samples per wavefront pass: large, so that the deep levels of a frame (few, slow,
     // incoherent rays) run once per frame rather than once per batch; the queues of a 2^27-sample
     // pass need ~50 GB at depth 5, well inside the 288 GB of HBM
@@ -303,9 +304,13 @@ int resolve_prof(rr_ctx* c) {
 
 int finish_stats(rr_ctx* c) {
     if (!c->stats_pending) return RR_OK;
-    HIPCHK(hipEventSynchronize(c->e1));
     float ms = 0.f;
-    HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
+    if (c->frame_timed) {
+        HIPCHK(hipEventSynchronize(c->e1));
+        HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
+    } else {
+        HIPCHK(sync_ctx(c));
+    }
     // the counters of the last render stay in HBM until the next one zeroes them: copy on demand
     // (a per-frame device-to-host copy behind a cross-stream wait blocks the host in HIP)
     HIPCHK(hipMemcpy(c->h_counters, c->stats_src ? c->stats_src : frame_counters(c, c->epoch), kCounterBytes,
@@ -521,7 +526,8 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
         HIPCHK(c->canvas.ensure(std::max<int64_t>(total, 1) * 3 * sizeof(double)));
         canvas = c->canvas.as<double>();
     }
-    HIPCHK(hipEventRecord(c->e0, st));
+    c->frame_timed = !(o->flags & RR_NO_FRAME_TIMING);
+    if (c->frame_timed) HIPCHK(hipEventRecord(c->e0, st));
     rr::LevelArgs A{};
     A.cam = dev_camera(cam);
     A.cam_affine = A.cam.inv[12] == 0.0 && A.cam.inv[13] == 0.0 && A.cam.inv[14] == 0.0 && A.cam.inv[15] == 1.0 &&
@@ -548,7 +554,7 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     else if (d_avg && !direct_avg)
         HIPCHK(rr::launch_aa(canvas, static_cast<double*>(d_avg), W, rows, o->aa, st,
                              c->profile ? &c->prof : nullptr));
-    HIPCHK(hipEventRecord(c->e1, st));
+    if (c->frame_timed) HIPCHK(hipEventRecord(c->e1, st));
     c->stats_pending = true;
     // C_SAMPLES is not incremented by the wavefront kernels; it is the level-0 event count
     c->last.samples = (uint64_t)total;

@@ -527,17 +527,6 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
             c.n1 = A.n12[2 * i];
             c.n2 = A.n12[2 * i + 1];
         }
-        pcol = material_color<CP>(S, m, hr.node, c.over);  // material.rs:77-80
-        RR_STAMPX(st0, 1);
-        if (PRE) {
-            double* pl = prelit_lds(S, LC);
-            for (int li = 0; li < S.n_lights; ++li) {
-                V3 amb, dsp;
-                light_terms(m, ldc(S.lights, li), pcol, c.over, c.eyev, c.normalv, amb, dsp);
-                const double v6[6] = {amb.x, amb.y, amb.z, dsp.x, dsp.y, dsp.z};
-                for (int k = 0; k < 6; ++k) pl[(li * 6 + k) * 256 + threadIdx.x] = v6[k];
-            }
-        }
         over = c.over;
         eyev = c.eyev;
         normalv = c.normalv;
@@ -602,6 +591,23 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
         if (pending) A.pending[slots[2]] = (int32_t)i;
     }
     RR_STAMP(cnt, 5);
+    // the surface colour and (PRE) every light's ambient / diffuse+specular terms, after the children
+    // are queued: point / under / reflectv and the child rays are dead by now, which keeps the
+    // pattern and `pow` code below the 128-VGPR budget without spilling
+    if (has_hit) {
+        const DevMaterial m = S.mats[mat];
+        pcol = material_color<CP>(S, m, hr.node, over);  // material.rs:77-80
+        RR_STAMPX(st0, 1);
+        if (PRE) {
+            double* pl = prelit_lds(S, LC);
+            for (int li = 0; li < S.n_lights; ++li) {
+                V3 amb, dsp;
+                light_terms(m, ldc(S.lights, li), pcol, over, eyev, normalv, amb, dsp);
+                const double v6[6] = {amb.x, amb.y, amb.z, dsp.x, dsp.y, dsp.z};
+                for (int k = 0; k < 6; ++k) pl[(li * 6 + k) * 256 + threadIdx.x] = v6[k];
+            }
+        }
+    }
     // surface = 0 + L0 + L1 + ... (scene.rs:159-166)
     V3 surface = mk(0, 0, 0);
 #ifdef RR_STAMPS
