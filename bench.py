@@ -198,6 +198,7 @@ def main():
     # flops of one step / (this kernel's time per step) == per-launch flops / average launch duration
     achieved = flops / (dom_ms / args.steps / 1e3) / 1e12 if dom_ms > 0 else 0.0
     traffic = None
+    entry = {}
     pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
     if os.path.exists(pmc):
         try:
@@ -206,7 +207,7 @@ def main():
             entry = per_kernel.get(dom) or (per_kernel.get("shade") if dom == "trace_shade" else None) or {}
             traffic = entry.get("hbm_bytes_per_launch")
         except Exception:
-            traffic = None
+            traffic, entry = None, {}
     # SURVEY §8(d) full-scan model for the same rays: what the reference's algorithm would execute
     per_ray = (FLOPS["sphere"] * counts["sphere"] + FLOPS["plane"] * counts["plane"] + FLOPS["group"] * counts["group"]
                + FLOPS["tri"] * counts["tri"])
@@ -232,6 +233,12 @@ def main():
                                          "flops_per_step": ref_flops,
                                          "model": "SURVEY §8(d) full scan (every ray tests every primitive; "
                                                   "triangles counted as if their group box were hit)"},
+                "valu_busy": {"frac": entry.get("valu_busy_frac"), "rocprof_kernel_ms":
+                              (entry["rocprof_avg_ns"] / 1e6 if entry.get("rocprof_avg_ns") else None),
+                              "source": entry.get("profile"),
+                              "model": "SQ_ACTIVE_INST_VALU (quad-cycles) x SQ_WAVES x 4 / (1024 SIMDs x 2.4 GHz x "
+                                       "rocprof mean launch time): the share of all SIMD cycles issuing vector "
+                                       "instructions, the bound this f64 kernel actually runs into"},
                 "note": "achieved = f64 flops the kernel executed: exact leaf tests after culling (SURVEY §8d model: "
                         "sphere 57, plane 13, triangle/group 45) + 250 per shade event for the shade kernel, / kernel "
                         "time; the f32 bundle/line culling that removes the other tests is overhead, not counted. Peak = MI355X FP64 vector = FP64 MFMA "

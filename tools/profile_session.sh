@@ -11,16 +11,17 @@ export TMPDIR=/tmp
 if [ "${SKIP_BUILD:-0}" != 1 ]; then
   python -c "import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1 || exit 1
 fi
-run() {  # name, timeout, rocprof args...
+STEPS=${STEPS:-50}  # the kernel-trace pass runs as many steps as the default bench line (clocks settle)
+run() {  # name, timeout, rocprof args...  (PSTEPS: steps of this pass)
   local name=$1 t=$2; shift 2
   echo "== $name ($(date +%T))"
   (cd /tmp && timeout -k 10 "$t" rocprofv3 "$@" -d "$OUT/$name" -o run --output-format csv -- \
-      python3 "$ROOTDIR/bench.py" --workload "$WL" --steps 5 --warmup 1 --no-cpu-baseline) > "$OUT/$name.log" 2>&1
+      python3 "$ROOTDIR/bench.py" --workload "$WL" --steps "${PSTEPS:-5}" --warmup "${PWARM:-1}" --no-cpu-baseline) > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "== $name rc=$rc"; tail -n 3 "$OUT/$name.log"
   return $rc
 }
-run kt 300 --kernel-trace --stats || exit 1
+PSTEPS=$STEPS PWARM=5 run kt 300 --kernel-trace --stats || exit 1
 run pmc_fetch 300 --pmc FETCH_SIZE || exit 1
 run pmc_write 300 --pmc WRITE_SIZE || exit 1
 run pmc_sq 300 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU || exit 1

@@ -17,10 +17,10 @@ def main(path):
             ("trace walk", r1[:, 4] - r1[:, 3], ok[ok]),
             ("-> prepare", r0[:, 5] - r1[:, 4], hit),
             ("prepare", r0[:, 0] - r0[:, 5], hit),
-            ("pattern", r0[:, 1] - r0[:, 0], hit),
-            ("prelit + schlick/children", r1[:, 1] - r0[:, 1], hit),
+            ("schlick / children", r1[:, 1] - r0[:, 0], hit),
             ("queue appends", r1[:, 5] - r1[:, 1], ok[ok]),
-            ("shadow prelude", r0[:, 2] - r1[:, 5], hit),
+            ("pattern", r0[:, 1] - r1[:, 5], hit),
+            ("prelit + shadow prelude", r0[:, 2] - r0[:, 1], hit),
             ("shadow bundle", r0[:, 3] - r0[:, 2], hit),
             ("shadow walk", r0[:, 4] - r0[:, 3], hit),
             ("light final", r1[:, 6] - r0[:, 4], hit),

@@ -11,6 +11,10 @@ import shutil
 import sys
 
 
+N_SIMDS = 256 * 4    # MI355X: 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
+CLOCK_HZ = 2.4e9     # max clock
+
+
 def per_kernel(path):
     rows = list(csv.DictReader(open(path)))
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -57,8 +61,15 @@ def main(src, tag, workload="c2_s1024"):
                              "sq_per_wave": {c: v / s["SQ_WAVES"] for c, v in s.items()
                                              if c.startswith("SQ_") and c != "SQ_WAVES"} if s.get("SQ_WAVES") else None,
                              "sq_waves": s.get("SQ_WAVES"), "grbm_gui_active": s.get("GRBM_GUI_ACTIVE")}
+        # VALU busy: SQ_ACTIVE_INST_VALU (quad-cycles per wave) summed over the launch's waves, over every
+        # SIMD's cycles of the launch (1024 SIMDs at the 2.4 GHz max clock: a lower bound on the fraction)
+        if s.get("SQ_WAVES") and s.get("SQ_ACTIVE_INST_VALU"):
+            busy = 4.0 * s["SQ_ACTIVE_INST_VALU"] / (N_SIMDS * CLOCK_HZ * float(r["AverageNs"]) * 1e-9)
+            out["kernels"][k]["valu_busy_frac"] = busy
     json.dump(out, open(f"profiles/{tag}_summary.json", "w"), indent=1)
-    json.dump({k: {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"]} for k, v in out["kernels"].items()},
+    json.dump({k: {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"], "valu_busy_frac": v.get("valu_busy_frac"),
+                   "rocprof_avg_ns": v["avg_ns"], "profile": f"profiles/{tag}_summary.json"}
+               for k, v in out["kernels"].items()},
               open(f"profiles/pmc_{workload}.json", "w"), indent=1)
     shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), f"profiles/{tag}_kernel_stats.csv")
     for p in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2"):
