@@ -143,8 +143,10 @@ struct DevScene {
     int32_t pad3;
 };
 // Node culls (16 B each) and chunk records (32 B each) are copied into LDS by every walking
-// workgroup when together they fit in this many bytes.
-constexpr int RR_LDS_CULL_BYTES = 40 * 1024;
+// workgroup when together they fit in this many bytes.  Small scenes gain from it (C5 2.5 %, C1
+// 1 %); at C2's 17 KB the per-workgroup staging costs more than the walks' L1/L2 reads of the few
+// candidate chunks save (global culls 0.173 vs LDS 0.175 ms per frame; C3 equal).
+constexpr int RR_LDS_CULL_BYTES = 8 * 1024;
 constexpr int RR_BUNDLE_MIN_NODES = 8;  // walks of scenes with at most this many nodes build no ray bundle
 
 // Per-launch counters (u64, zeroed by the host before each launch).
