@@ -274,3 +274,31 @@ def test_n1n2_and_refraction_scene(renderer, R):
     canvas, st = o.render(oracle.Oracle.camera(W, H, math.pi / 3, cam_t))
     assert st["rays"] > st["shade_events"]
     _compare(got, canvas, "nested glass")
+
+
+def test_device_render_without_frame_timing(renderer, R):
+    """rr_render_device into a device buffer (the bench / multi-GPU path), with and without the
+    per-frame HIP event pair (RR_NO_FRAME_TIMING): the same image as rr_render, and kernel_ms is 0
+    only when the events are off.  The buffer comes from the HIP runtime the library itself links
+    (torch ships its own runtime, which must initialise first when both are used: bench.py)."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    scene, _ = _yaml_pair("c2_s1024.yaml", 64, 40, 1)
+    renderer.upload(scene)
+    ref = renderer.render(scene.camera, aa=1)["avg"]
+    nbytes = ref.size * 8
+    for flags, timed in ((R._lib.RR_OUT_AVG, True), (R._lib.RR_OUT_AVG | R._lib.RR_NO_FRAME_TIMING, False)):
+        d = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(d), ctypes.c_size_t(nbytes)) == 0
+        try:
+            opts = R._lib.RenderOpts(1, 5, 0, 0, 0, 1, 8, flags)
+            renderer.render_device(scene.camera, opts, None, d.value, None)
+            st = renderer.last_stats()  # waits for the frame
+            out = np.empty_like(ref)
+            assert hip.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), d, ctypes.c_size_t(nbytes), 2) == 0
+        finally:
+            hip.hipFree(d)
+        assert np.array_equal(out, ref), flags
+        assert (st["kernel_ms"] > 0) == timed, st["kernel_ms"]
+        assert st["rays"] == 64 * 40
