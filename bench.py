@@ -49,8 +49,8 @@ def scene_counts(desc):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=50)  # a C2 step is ~0.18 ms: 50 + 10 frames settle the clocks
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c2_s1024", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-stride", type=int, default=1, help="CPU sample: one 8-row band in every STRIDE bands")
