@@ -67,7 +67,7 @@ struct rr_ctx {
     DBuf culls, chunks, nodes, groups, shapes, tris, mats, pats, lights, textures, texels;
     // workspace
     DBuf counters, lcount, hit, n12, n1n2, ev_a, ev_b, canvas, rays0, qout;
-    std::vector<DBuf> comb, pend;  // one per level
+    std::vector<DBuf> comb, comb_ext, pend;  // one per level (comb_ext: scenes with transparency)
     unsigned int* h_lcount = nullptr;  // pinned
     unsigned long long* h_counters = nullptr;
     // counters: [frame buffer 0][frame buffer 1][queries]; frames alternate (`epoch`), and each
@@ -173,11 +173,14 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
         for (int d = 0; d <= max_depth && n > 0; ++d) {
             if ((int)c->comb.size() <= d) {
                 c->comb.resize(d + 1);
+                c->comb_ext.resize(d + 1);
                 c->pend.resize(d + 1);
             }
             HIPCHK(c->hit.ensure(n * sizeof(rr::HitRec)));
             HIPCHK(c->n12.ensure(n * 2 * sizeof(double)));
             HIPCHK(c->comb[d].ensure(n * sizeof(rr::CombRec)));
+            const bool ext = c->host.has_transparent != 0;
+            if (ext) HIPCHK(c->comb_ext[d].ensure(n * sizeof(rr::CombExt)));
             HIPCHK(c->pend[d].ensure(n * sizeof(int32_t)));
             HIPCHK(c->n1n2.ensure(n * sizeof(int32_t)));
             // reflected/refracted rays need a reflective or transparent material: without one there is
@@ -202,6 +205,8 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             A.n12 = c->n12.as<double>();
             A.comb = c->comb[d].as<rr::CombRec>();
             A.parent_comb = d > 0 ? c->comb[d - 1].as<rr::CombRec>() : nullptr;
+            A.comb_ext = ext ? c->comb_ext[d].as<rr::CombExt>() : nullptr;
+            A.parent_ext = ext && d > 0 ? c->comb_ext[d - 1].as<rr::CombExt>() : nullptr;
             A.out = out;
             A.avg = avg;
             A.avg_f32 = avg_f32;
@@ -259,6 +264,9 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             C.pending = c->pend[d].as<int32_t>();
             C.comb = c->comb[d].as<rr::CombRec>();
             C.parent_comb = d > 0 ? c->comb[d - 1].as<rr::CombRec>() : nullptr;
+            const bool ext = c->host.has_transparent != 0;
+            C.comb_ext = ext ? c->comb_ext[d].as<rr::CombExt>() : nullptr;
+            C.parent_ext = ext && d > 0 ? c->comb_ext[d - 1].as<rr::CombExt>() : nullptr;
             C.out = out;
             C.avg = avg;
             C.avg_f32 = avg_f32;
@@ -377,6 +385,7 @@ void rr_destroy(rr_ctx* c) {
                     &c->lcount, &c->hit, &c->n12, &c->n1n2, &c->ev_a, &c->ev_b, &c->canvas, &c->rays0, &c->qout})
         b->release();
     for (auto& b : c->comb) b.release();
+    for (auto& b : c->comb_ext) b.release();
     for (auto& b : c->pend) b.release();
     for (hipEvent_t e : c->prof.pool) (void)hipEventDestroy(e);
     if (c->h_lcount) (void)hipHostFree(c->h_lcount);

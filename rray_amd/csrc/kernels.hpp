@@ -29,6 +29,8 @@ struct LevelArgs {
     double* n12;
     CombRec* comb;           // this level's pending sums (indexed by event)
     CombRec* parent_comb;    // level - 1 (children deliver into their parent's slot)
+    CombExt* comb_ext;       // refraction halves (null when no material is transparent)
+    CombExt* parent_ext;
     double* out;             // level 0: canvas / color_at results (3 doubles per local sample), or null
     void* avg;               // aa == 1: the averaged image written directly (canvas.rs:85-96 with aa = 1)
     int32_t avg_f32;         // avg holds floats (RR_OUT_AVG_F32)
@@ -50,6 +52,8 @@ struct CombArgs {
     const int32_t* pending;
     const CombRec* comb;
     CombRec* parent_comb;
+    const CombExt* comb_ext;  // as LevelArgs
+    CombExt* parent_ext;
     double* out;  // level 0: canvas (3 doubles per local sample), or null
     void* avg;    // as LevelArgs
     int32_t avg_f32;

@@ -301,7 +301,8 @@ __device__ __forceinline__ V3 shade_sum(V3 s, V3 a, V3 b, double refl, double tr
 // With aa == 1 the box average of canvas.rs:85-96 is r = 0.0; r += p; r /= 1.0, written here
 // directly (same operations) instead of through the canvas and aa_kernel.
 __device__ __forceinline__ void deliver(int32_t level, int64_t i, int32_t parent, int32_t slot, V3 v, double* out,
-                                        void* avg, int32_t avg_f32, CombRec* parent_comb, int64_t out_index) {
+                                        void* avg, int32_t avg_f32, CombRec* parent_comb, CombExt* parent_ext,
+                                        int64_t out_index) {
     if (level == 0) {
         if (out) {
             double* o = out + 3 * out_index;
@@ -325,13 +326,14 @@ __device__ __forceinline__ void deliver(int32_t level, int64_t i, int32_t parent
         }
         return;
     }
-    CombRec& p = parent_comb[parent];
-    if (slot) {
-        const double t = p.transp;
-        p.refr_res[0] = v.x * t;
-        p.refr_res[1] = v.y * t;
-        p.refr_res[2] = v.z * t;
+    if (slot) {  // a refracted child: the scene has transparency, so the parent has its CombExt
+        CombExt& e = parent_ext[parent];
+        const double t = e.transp;
+        e.refr_res[0] = v.x * t;
+        e.refr_res[1] = v.y * t;
+        e.refr_res[2] = v.z * t;
     } else {
+        CombRec& p = parent_comb[parent];
         const double t = p.refl;
         p.refl_res[0] = v.x * t;
         p.refl_res[1] = v.y * t;
@@ -641,17 +643,21 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
         cr.surf[1] = surface.y;
         cr.surf[2] = surface.z;
         cr.refl_res[0] = cr.refl_res[1] = cr.refl_res[2] = 0.0;
-        cr.refr_res[0] = cr.refr_res[1] = cr.refr_res[2] = 0.0;
         cr.refl = refl;
-        cr.transp = transp;
-        cr.R = R;
         cr.parent = parent;
         cr.flags = CF_HIT | (slot ? CF_REFRACT_CHILD : 0);
         A.comb[i] = cr;
+        if (A.comb_ext) {
+            CombExt ce;
+            ce.refr_res[0] = ce.refr_res[1] = ce.refr_res[2] = 0.0;
+            ce.transp = transp;
+            ce.R = R;
+            A.comb_ext[i] = ce;
+        }
     } else if (valid) {  // finished: color_at = shade_hit with black children, or black on a miss
         const V3 zero = mk(0.0, 0.0, 0.0);
         const V3 v = has_hit ? shade_sum(surface, zero, zero, refl, transp, R) : zero;
-        deliver(A.level, i, parent, slot, v, A.out, A.avg, A.avg_f32, A.parent_comb, ls0);
+        deliver(A.level, i, parent, slot, v, A.out, A.avg, A.avg_f32, A.parent_comb, A.parent_ext, ls0);
     }
     flush(cnt, A.counters, W_SHADOW);
     if (FUSED && (threadIdx.x & 63) == 0) {
@@ -668,11 +674,20 @@ __global__ void __launch_bounds__(256) combine_kernel(CombArgs C) {
     if (j >= C.n) return;
     const int64_t i = C.pending[j];
     const CombRec c = C.comb[i];
-    const V3 v = shade_sum(mk(c.surf[0], c.surf[1], c.surf[2]), mk(c.refl_res[0], c.refl_res[1], c.refl_res[2]),
-                           mk(c.refr_res[0], c.refr_res[1], c.refr_res[2]), c.refl, c.transp, c.R);
+    V3 b = mk(0.0, 0.0, 0.0);  // no transparency in the scene: refracted_color is black, transparency 0
+    double transp = 0.0, R = 0.0;
+    if (C.comb_ext) {
+        const CombExt e = C.comb_ext[i];
+        b = mk(e.refr_res[0], e.refr_res[1], e.refr_res[2]);
+        transp = e.transp;
+        R = e.R;
+    }
+    const V3 v = shade_sum(mk(c.surf[0], c.surf[1], c.surf[2]), mk(c.refl_res[0], c.refl_res[1], c.refl_res[2]), b,
+                           c.refl, transp, R);
     const uint32_t t = (uint32_t)(C.base + i);
     const int64_t oi = C.level == 0 ? (C.lrows > 0 ? tile_to_local_u32(t, (uint32_t)C.hs, (uint32_t)C.lrows) : t) : 0;
-    deliver(C.level, i, c.parent, (c.flags & CF_REFRACT_CHILD) ? 1 : 0, v, C.out, C.avg, C.avg_f32, C.parent_comb, oi);
+    deliver(C.level, i, c.parent, (c.flags & CF_REFRACT_CHILD) ? 1 : 0, v, C.out, C.avg, C.avg_f32, C.parent_comb,
+            C.parent_ext, oi);
 }
 
 // canvas.rs:85-96: r = 0.0; r += p (dy outer, dx inner); r /= aa*aa
