@@ -1,16 +1,23 @@
-"""Benchmark: Mpixel-samples/s of the MI355X render path on BASELINE.json's single-GPU config.
+"""Benchmark: Mpixel-samples/s of the MI355X render path (BASELINE.json metric).
 
-Workload (configs[1]): synthetic 1024-sphere grid + checker plane, point light, 1920x1080, AA=1
-(scenes/c2_s1024.yaml).  One step = one frame rendered to the AA-averaged f64 image in HBM
-(Camera::render + canvas.rs box average, before `as u8`).
+N = 1 (default): BASELINE configs[1] — synthetic 1024-sphere grid + checker plane, point light,
+1920x1080, AA=1 (scenes/c2_s1024.yaml).  One step = one frame rendered to the AA-averaged f64 image
+in HBM (Camera::render + canvas.rs box average, before `as u8`).  The line also carries the N = 1
+value of the multi-GPU workload (`scaling_anchor`), so the 1/2/4/8-GPU curve has its own anchor.
 
-With N ranks (torchrun, one process per GPU) there are two shardings:
-* --mode frames (default): the job renders a batch of N frames per step, one whole C2 frame per
-  rank, each kept resident on its rank (a renderer farm's frame sharding).  No data-path collective;
-  the process group only carries the barrier and the max-over-ranks timing ("scaling": "weak").
-* --mode tiles: one frame per step, its rows split in interleaved 8-row blocks; the tiles (f32) are
-  gathered to rank 0 with one RCCL gather per step, double-buffered so the gather of frame k overlaps
-  the render of frame k+1 ("scaling": "strong": the frame is fixed).  North_star's C3 layout.
+N > 1: BASELINE configs[2] — the same scene at 3840x2160 AA=3, reflective, depth 5 (C3), ONE frame
+per step split across the ranks in interleaved 8-row blocks (rank r renders output rows
+{y : (y // 8) % N == r}); each rank's f64 AA-averaged tile goes to rank 0 in one RCCL gather
+(torch.distributed backend "nccl" = RCCL over xGMI), double-buffered so the gather of frame k
+overlaps the render of frame k+1 ("scaling": "strong": the frame is fixed).  After the timed region
+rank 0 checks that the gathered frame is bit-identical to its own single-part render.
+`--mode frames` (opt-in) is the render-farm sharding: one whole frame per rank per step, no
+data-path collective ("scaling": "weak").
+
+`python bench.py --gpus N` with no WORLD_SIZE in the environment starts the N ranks itself (a
+torch.distributed.run child process, before anything touches the GPU); under torchrun it checks
+WORLD_SIZE == N.  `--dry-run` runs the same multi-rank logic on CPU (gloo, the CPU oracle as the
+tile renderer at a thumbnail size): a rehearsal of the distributed path, never a measurement.
 
 Also reported: the dominant kernel's roofline (HIP events on the render stream over the timed
 region), and the CPU oracle (test-infrastructure restatement of the reference) timed on a bounded
@@ -18,7 +25,10 @@ row sample on the host cores, whose rows are also compared with the GPU frame (m
 """
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,9 +43,12 @@ WORKLOADS = {  # name: (scene, W, H, aa, max_depth)
     "c5_area_light": ("c5_area_light.yaml", 1920, 1080, 2, 5),
     "c1_readme": ("c1_readme.yaml", 800, 600, 1, 5),
 }
+SINGLE_GPU_WORKLOAD = "c2_s1024"      # BASELINE configs[1]
+MULTI_GPU_WORKLOAD = "c3_s1024_reflect"  # BASELINE configs[2]
+BLOCK = 8  # output rows per interleaved block
 # SURVEY.md §8(d) algorithmic flop model (FMA = 2, sqrt/div = 1): per leaf test and per shade event
 FLOPS = {"sphere": 57, "plane": 13, "tri": 45, "group": 45, "shade": 250}
-FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP64 MFMA dense) peak, MI355X_MICROARCH.md / SURVEY §8d
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (256 CU x 2.4 GHz x 128 flop/clk), MI355X_MICROARCH.md
 
 
 def scene_counts(desc):
@@ -46,137 +59,178 @@ def scene_counts(desc):
             "objects": len(kinds)}
 
 
+def host_cpu_info():
+    """Cores this process may run on: the affinity mask, capped by a cgroup CPU quota when one is set
+    (on a shared GPU box nproc shows the whole machine), plus nproc and the lscpu model name."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except (OSError, subprocess.SubprocessError):
+        pass
+    usable = affinity if quota is None else max(1, min(affinity, int(math.floor(quota))))
+    return {"nproc": os.cpu_count(), "affinity": affinity, "cgroup_quota_cpus": quota, "model": model,
+            "threads_used": usable}
+
+
+def spawn_ranks(args):
+    """`bench.py --gpus N` outside torchrun: start N ranks (one process per GPU) as a child
+    torch.distributed.run, before any GPU call in this process; exit with its status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)  # a C2 step is ~0.18 ms: 50 + 10 frames settle the clocks
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="c2_s1024", choices=sorted(WORKLOADS))
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default: 50 for C2-sized frames, 10 for C3)")
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                    help=f"default: {SINGLE_GPU_WORKLOAD} at N=1, {MULTI_GPU_WORKLOAD} at N>1")
+    ap.add_argument("--mode", choices=("frames", "tiles"), default=None,
+                    help="multi-rank sharding: row tiles of one frame + RCCL gather (default at N>1) or whole "
+                         "frames per rank (opt-in render farm, weak scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-stride", type=int, default=1, help="CPU sample: one 8-row band in every STRIDE bands")
-    ap.add_argument("--mode", choices=("frames", "tiles"), default="frames",
-                    help="multi-rank sharding: whole frames per rank (weak) or row tiles of one frame + RCCL gather")
+    ap.add_argument("--cpu-stride", type=int, default=None,
+                    help="CPU sample: one 8-row band in every STRIDE bands (default sized to ~10-30 s)")
+    ap.add_argument("--no-anchor", action="store_true", help="N=1: skip the C3 scaling anchor")
     ap.add_argument("--kernel-events", choices=("separate", "timed"), default="separate",
                     help="per-launch HIP events for the roofline: over a second pass of K steps (default) or "
                          "inside the timed region")
     ap.add_argument("--force-dist", action="store_true",
                     help="rehearsal: run the multi-rank path (RCCL process group, pipelined gather) even at 1 rank")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the multi-rank path: gloo, oracle-rendered thumbnail tiles, no GPU")
     args = ap.parse_args()
 
-    import numpy as np
-    import torch
-    import torch.distributed as dist
-
-    rank = int(os.environ.get("RANK", "0"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    distributed = world > 1 or args.force_dist
-    if distributed:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    tiles = args.mode == "tiles"
-    multi = distributed and tiles  # row tiles + pipelined gather; frames mode renders like one GPU
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    mode = args.mode or ("tiles" if world > 1 else "frames")
+    workload = args.workload or (MULTI_GPU_WORKLOAD if world > 1 and mode == "tiles" else SINGLE_GPU_WORKLOAD)
+    if args.dry_run:
+        return dry_run(args, world, mode, workload)
+    return gpu_bench(args, world, mode, workload)
 
-    import rray_amd as R
 
-    scene_file, W, H, aa, depth = WORKLOADS[args.workload]
-    text = open(os.path.join(ROOT, "scenes", scene_file)).read()
-    scene = R.YamlScene(text, W, H, aa, obj_root=os.path.join(ROOT, "scenes"))
-    counts = scene_counts(scene.desc())
-    rend = R.Renderer(local)
-    rend.upload(scene)
-    cam = scene.camera
-    block = 8
-    part, nparts = (rank, world) if tiles else (0, 1)
-    rows = R.part_rows(H, part, nparts, block)
-    dev = torch.device("cuda", local)
-    from rray_amd import dist as rdist
-    if not multi:
-        # the AA-averaged f64 image (the drop-in's Canvas, before `as u8`)
-        tile = torch.zeros((len(rows), W, 3), dtype=torch.float64, device=dev)
-        opts = R._lib.RenderOpts(aa, depth, 0, 0, part, nparts, block, R._lib.RR_OUT_AVG | R._lib.RR_NO_FRAME_TIMING)
+class Session:
+    """One workload on this rank: the scene in HBM and a `step()` that renders one frame (frames mode /
+    one part) or this rank's tile of one frame plus the pipelined gather (tiles mode)."""
 
-        side = torch.cuda.Stream(dev) if os.environ.get("RRAY_BENCH_SIDE_STREAM") else None
+    def __init__(self, R, workload, dev, local, rank, world, tiles, distributed, rend):
+        import torch
+        from rray_amd import dist as rdist
 
-        def step():
-            stream = (side or torch.cuda.current_stream(dev)).cuda_stream
-            rend.render_device(cam, opts, None, tile.data_ptr(), stream)
-    else:
-        # tiles travel as f32 (the f64 average rounded once; far inside the 1e-5 gate), double-buffered
-        # so that rendering frame k+1 overlaps the RCCL gather of frame k
-        pipe = rdist.FramePipeline(H, W, 3, torch.float32, dev, block=block)
-        opts = R._lib.RenderOpts(aa, depth, 0, 0, rank, world, block,
-                                 R._lib.RR_OUT_AVG_F32 | R._lib.RR_NO_FRAME_TIMING)
-        render_stream = torch.cuda.Stream(dev)
+        self.workload = workload
+        self.scene_file, self.W, self.H, self.aa, self.depth = WORKLOADS[workload]
+        self.text = open(os.path.join(ROOT, "scenes", self.scene_file)).read()
+        self.scene = R.YamlScene(self.text, self.W, self.H, self.aa, obj_root=os.path.join(ROOT, "scenes"))
+        self.counts = scene_counts(self.scene.desc())
+        self.rend = rend
+        rend.upload(self.scene)
+        self.cam = self.scene.camera
+        self.dev = dev
+        self.tiles = tiles
+        self.multi = distributed and tiles
+        self.pipe = None
+        self.tile = None
+        part, nparts = (rank, world) if tiles else (0, 1)
+        rows = R.part_rows(self.H, part, nparts, BLOCK)
+        if not self.multi:
+            # the AA-averaged f64 image (the drop-in's Canvas, before `as u8`)
+            self.tile = torch.zeros((len(rows), self.W, 3), dtype=torch.float64, device=dev)
+            self.opts = R._lib.RenderOpts(self.aa, self.depth, 0, 0, part, nparts, BLOCK,
+                                          R._lib.RR_OUT_AVG | R._lib.RR_NO_FRAME_TIMING)
+            self.stream = torch.cuda.current_stream(dev)
+        else:
+            # f64 tiles (bit-identical to the 1-GPU image), double-buffered: rendering frame k+1 overlaps
+            # the RCCL gather of frame k
+            self.pipe = rdist.FramePipeline(self.H, self.W, 3, torch.float64, dev, block=BLOCK)
+            self.opts = R._lib.RenderOpts(self.aa, self.depth, 0, 0, rank, world, BLOCK,
+                                          R._lib.RR_OUT_AVG | R._lib.RR_NO_FRAME_TIMING)
+            self.stream = torch.cuda.Stream(dev)
 
-        trace_host = {} if os.environ.get("RRAY_BENCH_TRACE") else None
+    def step(self):
+        import torch
 
-        def lap(name, t):
-            if trace_host is None:
-                return t
-            now = time.perf_counter()
-            trace_host[name] = trace_host.get(name, 0.0) + now - t
-            return now
+        if not self.multi:
+            self.rend.render_device(self.cam, self.opts, None, self.tile.data_ptr(), self.stream.cuda_stream)
+            return
+        i, buf, prev = self.pipe.acquire()
+        with torch.cuda.stream(self.stream):
+            if prev is not None:
+                prev.wait()  # the gather that last read this buffer
+            self.rend.render_device(self.cam, self.opts, None, buf.data_ptr(), self.stream.cuda_stream)
+        torch.cuda.current_stream(self.dev).wait_stream(self.stream)
+        self.pipe.submit(i)
 
-        def step():
-            t = time.perf_counter()
-            i, buf, prev = pipe.acquire()
-            with torch.cuda.stream(render_stream):
-                if prev is not None:
-                    prev.wait()  # the gather that last read this buffer
-                t = lap("prev.wait", t)
-                rend.render_device(cam, opts, None, buf.data_ptr(), render_stream.cuda_stream)
-                t = lap("render_device", t)
-            torch.cuda.current_stream(dev).wait_stream(render_stream)
-            t = lap("wait_stream", t)
-            pipe.submit(i)
-            lap("submit", t)
-        tile = None
+    def frame(self):
+        """The latest assembled AA-averaged frame (rank 0 in tiles mode), as a CPU numpy array."""
+        if self.multi:
+            return self.pipe.frame.cpu().numpy() if self.pipe.frame is not None else None
+        return self.tile.cpu().numpy()
 
+
+def timed_loop(sess, steps, warmup, distributed, dist, torch, kernel_events="separate"):
     def sync():
-        if multi:
-            pipe.drain()
-        torch.cuda.synchronize(dev)
+        if sess.multi:
+            sess.pipe.drain()
+        torch.cuda.synchronize(sess.dev)
         if distributed:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        step()
+    for _ in range(warmup):
+        sess.step()
     sync()
-    if multi and trace_host is not None:
-        trace_host.clear()
     # Per-launch HIP events cost ~5 % of a C2 frame, so by default the timed region runs without them
     # and the dominant kernel's launches are timed with HIP events (render stream) over a second pass
     # of the same K steps right after it; --kernel-events timed puts them inside the timed region.
-    in_region = args.kernel_events == "timed"
-    rend.kernel_profile(in_region)
+    in_region = kernel_events == "timed"
+    sess.rend.kernel_profile(in_region)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for _ in range(steps):
+        sess.step()
     t_enq = time.perf_counter()
-    if world > 1 or args.force_dist:
-        if trace_host is not None:
-            print("host ms/step:", {k: round(v / args.steps * 1e3, 4) for k, v in trace_host.items()}, file=sys.stderr)
     sync()
     t1 = time.perf_counter()
     if not in_region:
-        rend.kernel_profile(True)
-        for _ in range(args.steps):
-            step()
+        sess.rend.kernel_profile(True)
+        for _ in range(steps):
+            sess.step()
         sync()
-    ktimes = rend.kernel_times()
-    rend.kernel_profile(False)
-    stats = rend.last_stats()
+    ktimes = sess.rend.kernel_times()
+    sess.rend.kernel_profile(False)
+    stats = sess.rend.last_stats()
     elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=sess.dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    samples_per_frame = W * H * aa * aa
-    frames_per_step = world if not tiles else 1  # frames mode: every rank renders a whole frame per step
-    value = frames_per_step * samples_per_frame * args.steps / elapsed / 1e6
+    return elapsed, (t_enq - t0), ktimes, stats, in_region
 
-    # roofline of the dominant kernel (rank 0's measurements)
+
+def roofline_of(sess, ktimes, stats, steps, in_region):
     ktimes = {k: v for k, v in ktimes.items() if v[1]}
     if not ktimes:
         ktimes = {"none": (0.0, 1)}
@@ -184,105 +238,161 @@ def main():
     dom_ms, dom_n = ktimes[dom]
     # f64 flops this kernel executed in the last step: the exact leaf tests its walks ran after culling
     # (trace / n1n2 walks; the shade kernel runs the is_shadowed walks) + the shade-event model
-    if dom == "trace":
-        flops = stats["exact_flops"][0]
-    elif dom == "n1n2":
-        flops = stats["exact_flops"][2]
-    elif dom == "shade":
-        flops = stats["exact_flops"][1] + stats["shade_events"] * FLOPS["shade"]
-    elif dom == "trace_shade":  # fused: closest-hit walk + shading + shadow walks
-        flops = stats["exact_flops"][0] + stats["exact_flops"][1] + stats["shade_events"] * FLOPS["shade"]
-    else:
-        flops = 0
-    launches_per_frame = dom_n / args.steps
+    ef = stats["exact_flops"]
+    flops = {"trace": ef[0], "n1n2": ef[2], "shade": ef[1] + stats["shade_events"] * FLOPS["shade"],
+             "trace_shade": ef[0] + ef[1] + stats["shade_events"] * FLOPS["shade"]}.get(dom, 0)
+    launches_per_step = dom_n / steps
     # flops of one step / (this kernel's time per step) == per-launch flops / average launch duration
-    achieved = flops / (dom_ms / args.steps / 1e3) / 1e12 if dom_ms > 0 else 0.0
-    traffic = None
-    entry = {}
-    pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
+    achieved = flops / (dom_ms / steps / 1e3) / 1e12 if dom_ms > 0 else 0.0
+    traffic, entry = None, {}
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{sess.workload}.json")
     if os.path.exists(pmc):
         try:
             per_kernel = json.load(open(pmc))
             # the fused trace+shade launch is the shade_kernel<..., FUSED> instantiation in rocprof's naming
             entry = per_kernel.get(dom) or (per_kernel.get("shade") if dom == "trace_shade" else None) or {}
             traffic = entry.get("hbm_bytes_per_launch")
-        except Exception:
+        except (OSError, ValueError):
             traffic, entry = None, {}
+    c = sess.counts
     # SURVEY §8(d) full-scan model for the same rays: what the reference's algorithm would execute
-    per_ray = (FLOPS["sphere"] * counts["sphere"] + FLOPS["plane"] * counts["plane"] + FLOPS["group"] * counts["group"]
-               + FLOPS["tri"] * counts["tri"])
-    if dom == "trace":
-        ref_flops = stats["rays"] * per_ray
-    elif dom == "n1n2":
-        ref_flops = stats["n1n2_scans"] * per_ray
-    elif dom == "shade":
-        ref_flops = stats["shadow_rays"] * per_ray + stats["shade_events"] * FLOPS["shade"]
-    elif dom == "trace_shade":
-        ref_flops = (stats["rays"] + stats["shadow_rays"]) * per_ray + stats["shade_events"] * FLOPS["shade"]
-    else:
-        ref_flops = 0
-    ref_tf = ref_flops / (dom_ms / args.steps / 1e3) / 1e12 if dom_ms > 0 else 0.0
-    roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": traffic, "kernel": dom,
-                "kernel_ms": round(dom_ms / dom_n, 4),
-                "kernel_timing": "HIP events around every launch on the render stream, "
-                                 + ("inside the timed region" if in_region else
-                                    f"over a second pass of the same {args.steps} steps after the timed region"), "launches_per_step": launches_per_frame,
-                "flops_per_launch": flops / launches_per_frame,
-                "reference_equivalent": {"tflops": round(ref_tf, 2), "frac": round(ref_tf / FP64_PEAK_TFLOPS, 3),
-                                         "flops_per_step": ref_flops,
-                                         "model": "SURVEY §8(d) full scan (every ray tests every primitive; "
-                                                  "triangles counted as if their group box were hit)"},
-                "valu_busy": {"frac": entry.get("valu_busy_frac"), "rocprof_kernel_ms":
-                              (entry["rocprof_avg_ns"] / 1e6 if entry.get("rocprof_avg_ns") else None),
-                              "source": entry.get("profile"),
-                              "model": "SQ_ACTIVE_INST_VALU (quad-cycles) x SQ_WAVES x 4 / (1024 SIMDs x 2.4 GHz x "
-                                       "rocprof mean launch time): the share of all SIMD cycles issuing vector "
-                                       "instructions, the bound this f64 kernel actually runs into"},
-                "note": "achieved = f64 flops the kernel executed: exact leaf tests after culling (SURVEY §8d model: "
-                        "sphere 57, plane 13, triangle/group 45) + 250 per shade event for the shade kernel, / kernel "
-                        "time; the f32 bundle/line culling that removes the other tests is overhead, not counted. Peak = MI355X FP64 vector = FP64 MFMA "
-                        "dense 78.6 TF; bit-parity forbids FMA contraction (DESIGN.md §4)"}
+    per_ray = FLOPS["sphere"] * c["sphere"] + FLOPS["plane"] * c["plane"] + FLOPS["group"] * c["group"] + FLOPS["tri"] * c["tri"]
+    ref_flops = {"trace": stats["rays"] * per_ray, "n1n2": stats["n1n2_scans"] * per_ray,
+                 "shade": stats["shadow_rays"] * per_ray + stats["shade_events"] * FLOPS["shade"],
+                 "trace_shade": (stats["rays"] + stats["shadow_rays"]) * per_ray + stats["shade_events"] * FLOPS["shade"]
+                 }.get(dom, 0)
+    ref_tf = ref_flops / (dom_ms / steps / 1e3) / 1e12 if dom_ms > 0 else 0.0
+    return {"bound": "valu_fp64", "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": traffic, "kernel": dom,
+            "kernel_ms": round(dom_ms / dom_n, 4),
+            "kernel_timing": "HIP events around every launch on the render stream, "
+                             + ("inside the timed region" if in_region else
+                                f"over a second pass of the same {steps} steps after the timed region"),
+            "launches_per_step": launches_per_step,
+            "flops_per_launch": flops / launches_per_step if launches_per_step else 0,
+            "reference_equivalent": {"tflops": round(ref_tf, 2), "frac": round(ref_tf / FP64_PEAK_TFLOPS, 3),
+                                     "flops_per_step": ref_flops,
+                                     "model": "SURVEY §8(d) full scan (every ray tests every primitive; "
+                                              "triangles counted as if their group box were hit)"},
+            "valu_busy": {"frac": entry.get("valu_busy_frac"), "rocprof_kernel_ms":
+                          (entry["rocprof_avg_ns"] / 1e6 if entry.get("rocprof_avg_ns") else None),
+                          "source": entry.get("profile"),
+                          "model": "SQ_ACTIVE_INST_VALU (quad-cycles) x SQ_WAVES x 4 / (1024 SIMDs x 2.4 GHz x "
+                                   "rocprof mean launch time): the share of all SIMD cycles issuing vector "
+                                   "instructions"},
+            "note": "bound = FP64 vector ALU (no MFMA: no dense contraction on this path; HBM idle). achieved = f64 "
+                    "flops the kernel executed: exact leaf tests after culling (SURVEY §8d model: sphere 57, plane 13, "
+                    "triangle/group 45) + 250 per shade event, / kernel time; the f32 bundle/line culling that removes "
+                    "the other tests is overhead, not counted. Peak = MI355X FP64 vector 78.6 TF; bit-parity forbids "
+                    "FMA contraction (DESIGN.md §4)"}
 
-    cpu = None
-    parity = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        import oracle
-        from oracle.scene_yaml import build_from_yaml
 
-        threads = min(16, os.cpu_count() or 1)
-        o, ocam = build_from_yaml(text, W, H, aa, obj_root=os.path.join(ROOT, "scenes"))
-        tc = time.perf_counter()
-        canvas, _ = o.render(ocam, max_depth=depth, threads=threads, band=block * aa, band_stride=args.cpu_stride)
-        dt = time.perf_counter() - tc
-        sel = np.array([y for y in range(H * aa) if (y // (block * aa)) % args.cpu_stride == 0])
-        cpu_samples = len(sel) * W * aa
-        cpu = {"value": round(cpu_samples / dt / 1e6, 5), "unit": "Mpixel-samples/s", "cores": threads, "kind": "port",
-               "sample": f"oracle (C++ restatement, reference structure: per-object inverse, full xs list + stable "
-                         f"sort, recursion) on {len(sel) // aa} of {H} output rows (one {block}-row band in every "
-                         f"{args.cpu_stride}), {cpu_samples} samples, {dt:.1f}s"}
-        avg = o.aa_average(np.nan_to_num(canvas), aa)
-        out_rows = sorted(set(int(y) // aa for y in sel))
-        gpu_img = tile.cpu().numpy() if not multi else pipe.frame.double().cpu().numpy()
-        parity = {"rows_checked": len(out_rows),
-                  "max_abs_diff": float(np.max(np.abs(gpu_img[out_rows] - avg[out_rows]))),
-                  "bit_exact_frac": float(np.mean(gpu_img[out_rows] == avg[out_rows]))}
+def default_cpu_stride(workload):
+    # bounded oracle sample (~10-30 s on 16 cores): every band for the small frames, one 8-row band in
+    # every K for the big ones
+    return {"c2_s1024": 1, "c1_readme": 1, "c4_teapot": 4, "c5_area_light": 16, "c3_s1024_reflect": 16}[workload]
 
+
+def cpu_leg(sess, args, gpu_img):
+    """The oracle on the host cores over a bounded band sample of the same frame, and the GPU frame's
+    rows compared with it (test-infrastructure checker; nothing here is measured as the product)."""
+    import numpy as np
+
+    import oracle
+    from oracle.scene_yaml import build_from_yaml
+
+    info = host_cpu_info()
+    threads = info["threads_used"]
+    stride = args.cpu_stride or default_cpu_stride(sess.workload)
+    W, H, aa = sess.W, sess.H, sess.aa
+    o, ocam = build_from_yaml(sess.text, W, H, aa, obj_root=os.path.join(ROOT, "scenes"))
+    tc = time.perf_counter()
+    canvas, _ = o.render(ocam, max_depth=sess.depth, threads=threads, band=BLOCK * aa, band_stride=stride)
+    dt = time.perf_counter() - tc
+    sel = np.array([y for y in range(H * aa) if (y // (BLOCK * aa)) % stride == 0])
+    cpu_samples = len(sel) * W * aa
+    cpu = {"value": round(cpu_samples / dt / 1e6, 5), "unit": "Mpixel-samples/s", "cores": threads, "kind": "port",
+           "host": info,
+           "sample": f"oracle (C++ restatement, reference structure: per-object inverse, full xs list + stable "
+                     f"sort, recursion; {threads} threads) on {len(sel) // aa} of {H} output rows of "
+                     f"{sess.workload} (one {BLOCK}-row band in every {stride}), {cpu_samples} samples, {dt:.1f}s"}
+    avg = o.aa_average(np.nan_to_num(canvas), aa)
+    del canvas
+    out_rows = sorted(set(int(y) // aa for y in sel))
+    d = np.abs(gpu_img[out_rows] - avg[out_rows])
+    parity = {"workload": sess.workload, "rows_checked": len(out_rows), "max_abs_diff": float(np.max(d)),
+              "bit_exact_frac": float(np.mean(gpu_img[out_rows] == avg[out_rows])),
+              "u8_pixels_different": int(np.sum(np.any(o.quantize(gpu_img[out_rows]) != o.quantize(avg[out_rows]),
+                                                        axis=-1)))}
+    return cpu, parity
+
+
+def gpu_bench(args, world, mode, workload):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    distributed = world > 1 or args.force_dist
+    if distributed:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    tiles = mode == "tiles"
+    import rray_amd as R
+
+    dev = torch.device("cuda", local)
+    rend = R.Renderer(local)
+    sess = Session(R, workload, dev, local, rank, world, tiles, distributed, rend)
+    big = WORKLOADS[workload][1] * WORKLOADS[workload][2] * WORKLOADS[workload][3] ** 2 > 20_000_000
+    steps = args.steps if args.steps is not None else (10 if big else 50)
+    warmup = args.warmup if args.warmup is not None else (2 if big else 10)
+    elapsed, t_enq, ktimes, stats, in_region = timed_loop(sess, steps, warmup, distributed, dist, torch,
+                                                          args.kernel_events)
+    samples_per_frame = sess.W * sess.H * sess.aa * sess.aa
+    frames_per_step = world if not tiles else 1  # frames mode: every rank renders a whole frame per step
+    value = frames_per_step * samples_per_frame * steps / elapsed / 1e6
+    roofline = roofline_of(sess, ktimes, stats, steps, in_region)
+
+    # tiles: the gathered frame must be bit-identical to one part rendering the whole frame (§8(e))
+    identity = None
+    if sess.multi:
+        gathered = sess.frame() if rank == 0 else None
+        if rank == 0:
+            full = rend.render(sess.cam, aa=sess.aa, max_depth=sess.depth)["avg"]
+            identity = {"bit_identical_to_1_part": bool(np.array_equal(gathered, full)),
+                        "max_abs_diff": float(np.max(np.abs(gathered - full)))}
+        dist.barrier()
+
+    cpu = parity = anchor = None
+    if rank == 0 and world == 1 and not args.force_dist:
+        if not args.no_cpu_baseline:
+            cpu, parity = cpu_leg(sess, args, sess.frame())
+        if not args.no_anchor and workload != MULTI_GPU_WORKLOAD:
+            # the N = 1 point of the multi-GPU curve: C3 as one part on this GPU
+            a = Session(R, MULTI_GPU_WORKLOAD, dev, local, 0, 1, True, False, rend)
+            a_el, _, _, _, _ = timed_loop(a, 5, 1, False, dist, torch)
+            a_samples = a.W * a.H * a.aa * a.aa
+            anchor = {"workload": MULTI_GPU_WORKLOAD, "n_gpus": 1, "value": round(a_samples * 5 / a_el / 1e6, 3),
+                      "ms_per_step": round(a_el / 5 * 1e3, 4), "steps": 5, "warmup": 1,
+                      "note": "N=1 value of the N>1 workload (row tiles with nparts=1), for the scaling curve"}
     if rank == 0:
+        par = (f"row-tiles x{world} + rccl gather (f64 tiles, pipelined)" if world > 1 or sess.multi else
+               "single GPU, whole frame") if tiles else \
+            f"frame-parallel x{world} (one whole frame per rank per step, no data-path collective)"
         line = {"metric": METRIC, "value": round(value, 3), "unit": "Mpixel-samples/s", "n_gpus": world,
-                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                "steps": steps, "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 4),
                 "higher_is_better": True,
                 "scaling": "strong" if tiles else "weak", "vs_baseline": None, "dtype": "f64",
                 "data": "synthetic (scenes/make_scenes.py, seeded)",
-                "config": {"workload": args.workload, "scene": scene_file, "width": W, "height": H, "aa": aa,
-                           "max_depth": depth, "samples_per_step": samples_per_frame, "objects": counts["objects"],
-                           "frames_per_step": frames_per_step,
-                           "parallelism": (f"row-tiles x{world}" + (" + pipelined rccl gather (f32 tiles)"
-                                                                    if world > 1 else "")) if tiles else
-                           f"frame-parallel x{world} (one whole frame per rank per step, no data-path collective)"},
+                "config": {"workload": workload, "scene": sess.scene_file, "width": sess.W, "height": sess.H,
+                           "aa": sess.aa, "max_depth": sess.depth, "samples_per_step": samples_per_frame,
+                           "objects": sess.counts["objects"], "frames_per_step": frames_per_step,
+                           "parallelism": par},
                 "roofline": roofline, "cpu_baseline": cpu, "parity_sample": parity,
-                "kernels_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in ktimes.items() if v[1]},
-                "host_enqueue_ms_per_step": round((t_enq - t0) / args.steps * 1e3, 4),
+                "tile_identity": identity, "scaling_anchor": anchor,
+                "kernels_ms_per_step": {k: round(v[0] / steps, 4) for k, v in ktimes.items() if v[1]},
+                "host_enqueue_ms_per_step": round(t_enq / steps * 1e3, 4),
                 "stats_last_step": {k: stats[k] for k in ("rays", "shadow_rays", "shade_events", "n1n2_scans",
                                                           "prim_tests", "exact_flops", "wave_visits")}}
         print(json.dumps(line), flush=True)
@@ -290,6 +400,80 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     rend.close()
+
+
+def dry_run(args, world, mode, workload):
+    """CPU rehearsal of the multi-rank bench (gloo): same spawn, world check, row partition, pipelined
+    gather and max-over-ranks timing; each rank's tile is rendered by the CPU oracle at a thumbnail size
+    (test infrastructure standing in for the GPU).  Not a measurement."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from oracle.scene_yaml import build_from_yaml
+    from rray_amd import dist as rdist
+
+    rank = int(os.environ.get("RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        dist.init_process_group("gloo")
+    tiles = mode == "tiles"
+    scene_file, W0, H0, aa, depth = WORKLOADS[workload]
+    W, H = 96, 54
+    text = open(os.path.join(ROOT, "scenes", scene_file)).read()
+    o, cam = build_from_yaml(text, W, H, aa, obj_root=os.path.join(ROOT, "scenes"))
+    steps = args.steps or 2
+    part, nparts = (rank, world) if tiles else (0, 1)
+    rows = rdist.tile_rows(H, part, nparts, BLOCK)
+
+    def render_tile(out):
+        canvas, _ = o.render(cam, max_depth=depth, threads=2, band=BLOCK * aa, band_stride=nparts, band_phase=part)
+        avg = o.aa_average(np.nan_to_num(canvas), aa)
+        out[: len(rows)] = torch.from_numpy(avg[rows])
+
+    pipe = rdist.FramePipeline(H, W, 3, torch.float64, torch.device("cpu"), block=BLOCK) if (tiles and distributed) \
+        else None
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        if pipe is not None:
+            i, buf, prev = pipe.acquire()
+            if prev is not None:
+                prev.wait()
+            render_tile(buf)
+            pipe.submit(i)
+        else:
+            render_tile(torch.zeros((len(rows), W, 3), dtype=torch.float64))
+    if pipe is not None:
+        pipe.drain()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    identity = None
+    if rank == 0 and pipe is not None:
+        full, _ = o.render(cam, max_depth=depth, threads=2)
+        identity = {"bit_identical_to_1_part": bool(np.array_equal(pipe.frame.numpy(), o.aa_average(full, aa)))}
+    if rank == 0:
+        frames_per_step = world if not tiles else 1
+        line = {"metric": METRIC, "value": round(frames_per_step * W * H * aa * aa * steps / elapsed / 1e6, 6),
+                "unit": "Mpixel-samples/s", "n_gpus": world, "steps": steps, "warmup": 0,
+                "ms_per_step": round(elapsed / steps * 1e3, 3), "higher_is_better": True,
+                "scaling": "strong" if tiles else "weak", "vs_baseline": None, "dtype": "f64",
+                "data": "synthetic (scenes/make_scenes.py, seeded)",
+                "dry_run": f"gloo on CPU, CPU-oracle tiles at {W}x{H} (not {W0}x{H0}): a rehearsal, not a measurement",
+                "config": {"workload": workload, "scene": scene_file, "width": W, "height": H, "aa": aa,
+                           "max_depth": depth, "frames_per_step": frames_per_step,
+                           "parallelism": (f"row-tiles x{world} + rccl gather (f64 tiles, pipelined)" if tiles else
+                                           f"frame-parallel x{world} (one whole frame per rank per step, "
+                                           "no data-path collective)")},
+                "tile_identity": identity}
+        print(json.dumps(line), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

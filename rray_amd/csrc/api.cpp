@@ -68,7 +68,6 @@ struct rr_ctx {
     // workspace
     DBuf counters, lcount, hit, n12, n1n2, ev_a, ev_b, canvas, rays0, qout;
     std::vector<DBuf> comb, comb_ext, pend;  // one per level (comb_ext: scenes with transparency)
-    unsigned int* h_lcount = nullptr;  // pinned
     unsigned long long* h_counters = nullptr;
     // counters: [frame buffer 0][frame buffer 1][queries]; frames alternate (`epoch`), and each
     // frame's first kernels zero the other buffer for the next frame
@@ -85,6 +84,9 @@ struct rr_ctx {
     // incoherent rays) run once per frame rather than once per batch; the queues of a 2^27-sample
     // pass need ~50 GB at depth 5, well inside the 288 GB of HBM
     int64_t batch = (int64_t)1 << 27;
+    // bytes the worst-case recursion queues of one batch may take (run_levels shrinks the batch to fit;
+    // half of the free HBM at context creation, RRAY_QUEUE_BUDGET_MB overrides)
+    size_t queue_budget = (size_t)32 << 30;
     // per-kernel timing (rr_kernel_times)
     bool profile = false;
     rr::KernelProf prof;
@@ -160,35 +162,75 @@ unsigned long long* frame_counters(rr_ctx* c, int k) {
     return c->counters.as<unsigned long long>() + (size_t)k * rr::RR_CNT_SLOTS * rr::RR_CNT_STRIDE;
 }
 
+// Worst-case queue bytes of a batch of nb level-0 events: every shading event queues max_children
+// children (k), so level d holds at most nb * k^d events.  The levels are launched for that capacity
+// and read their live counts from HBM (no host round trip between levels).
+struct LevelPlan {
+    int64_t cap[RR_MAX_DEPTH + 1];  // capacity per level
+    int levels;                     // levels launched (depth + 1, or 1 without secondary rays)
+    int64_t ev_cap[2];              // ev_a (odd levels), ev_b (even levels >= 2)
+    int64_t max_cap;
+    size_t bytes;
+};
+LevelPlan plan_levels(int64_t nb, int k, int max_depth, bool ext) {
+    LevelPlan p{};
+    int64_t w = nb;
+    for (int d = 0; d <= max_depth; ++d) {
+        p.cap[d] = w;
+        p.levels = d + 1;
+        p.max_cap = std::max(p.max_cap, w);
+        const bool kids = d < max_depth && k > 0;
+        if (!kids) break;
+        p.bytes += (size_t)w * (sizeof(rr::CombRec) + (ext ? sizeof(rr::CombExt) : 0) + sizeof(int32_t));
+        w *= k;
+        int64_t& e = p.ev_cap[d % 2];  // level d+1 lands in ev_a when d is even
+        e = std::max(e, w);
+    }
+    p.bytes += (size_t)p.max_cap * (sizeof(rr::HitRec) + 2 * sizeof(double) + sizeof(int32_t));
+    p.bytes += (size_t)(p.ev_cap[0] + p.ev_cap[1]) * sizeof(rr::Event);
+    return p;
+}
+
 int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max_depth, double* out, hipStream_t st,
                void* avg = nullptr, int32_t avg_f32 = 0) {
-    const int64_t B = std::max<int64_t>(1, c->batch);
+    const int k = c->host.max_children;
+    const bool ext = c->host.has_transparent != 0;
+    // batch: at most c->batch camera samples, shrunk (power-of-two steps, tile-aligned) until the
+    // worst-case queues fit the context's budget and every event index fits in int32
+    int64_t B = std::max<int64_t>(64, std::min<int64_t>(c->batch, total));
+    for (;;) {
+        const LevelPlan p = plan_levels(B, k, max_depth, ext);
+        const int64_t last = p.cap[p.levels - 1];
+        if (B <= 4096 || (p.bytes <= c->queue_budget && last < ((int64_t)1 << 31) && p.max_cap < ((int64_t)1 << 31)))
+            break;
+        B = std::max<int64_t>(4096, (B / 2) & ~(int64_t)63);
+    }
+    const LevelPlan P = plan_levels(B, k, max_depth, ext);
+    if (P.max_cap >= ((int64_t)1 << 31)) return fail(RR_E_LIMIT, "recursion queues exceed 2^31 events (lower max_depth)");
+    if ((int)c->comb.size() < P.levels) {
+        c->comb.resize(P.levels);
+        c->comb_ext.resize(P.levels);
+        c->pend.resize(P.levels);
+    }
+    HIPCHK(c->hit.ensure(P.max_cap * sizeof(rr::HitRec)));
+    HIPCHK(c->n12.ensure(P.max_cap * 2 * sizeof(double)));
+    HIPCHK(c->n1n2.ensure(P.max_cap * sizeof(int32_t)));
+    for (int d = 0; d + 1 < P.levels; ++d) {
+        HIPCHK(c->comb[d].ensure(P.cap[d] * sizeof(rr::CombRec)));
+        if (ext) HIPCHK(c->comb_ext[d].ensure(P.cap[d] * sizeof(rr::CombExt)));
+        HIPCHK(c->pend[d].ensure(P.cap[d] * sizeof(int32_t)));
+    }
+    if (P.ev_cap[0]) HIPCHK(c->ev_a.ensure(P.ev_cap[0] * sizeof(rr::Event)));
+    if (P.ev_cap[1]) HIPCHK(c->ev_b.ensure(P.ev_cap[1] * sizeof(rr::Event)));
+    unsigned int* lc = c->lcount.as<unsigned int>();
     for (int64_t base = 0; base < total; base += B) {
         const int64_t nb = std::min(B, total - base);
-        std::vector<int64_t> level_n;
-        int64_t n = nb;
-        DBuf* cur_ev = nullptr;
-        DBuf* nxt_ev = &c->ev_a;
-        std::vector<int64_t> level_pend;
-        for (int d = 0; d <= max_depth && n > 0; ++d) {
-            if ((int)c->comb.size() <= d) {
-                c->comb.resize(d + 1);
-                c->comb_ext.resize(d + 1);
-                c->pend.resize(d + 1);
-            }
-            HIPCHK(c->hit.ensure(n * sizeof(rr::HitRec)));
-            HIPCHK(c->n12.ensure(n * 2 * sizeof(double)));
-            HIPCHK(c->comb[d].ensure(n * sizeof(rr::CombRec)));
-            const bool ext = c->host.has_transparent != 0;
-            if (ext) HIPCHK(c->comb_ext[d].ensure(n * sizeof(rr::CombExt)));
-            HIPCHK(c->pend[d].ensure(n * sizeof(int32_t)));
-            HIPCHK(c->n1n2.ensure(n * sizeof(int32_t)));
-            // reflected/refracted rays need a reflective or transparent material: without one there is
-            // no level 1, and no host round trip for the child count
-            const bool children_possible = d < max_depth && c->host.has_secondary;
-            if (children_possible) HIPCHK(nxt_ev->ensure(2 * n * sizeof(rr::Event)));
-            if (children_possible || c->host.has_transparent)  // queue counters (appends, n1/n2 list)
-                HIPCHK(hipMemsetAsync(c->lcount.p, 0, rr::LC_COUNT * sizeof(unsigned int), st));
+        const LevelPlan p = plan_levels(nb, k, max_depth, ext);
+        // per-level queue counters [level][LC_*], zeroed once per batch (appends, pending, n1/n2 lists)
+        if (p.levels > 1 || ext)
+            HIPCHK(hipMemsetAsync(lc, 0, (size_t)p.levels * rr::LC_COUNT * sizeof(unsigned int), st));
+        for (int d = 0; d < p.levels; ++d) {
+            const bool children_possible = d + 1 < p.levels;
             rr::LevelArgs A = base_args;
             A.base = base;
             // level-0 index math: magic divisors, and the wave-uniform tile path when every tile is
@@ -199,21 +241,24 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             A.tiles_per_row = (uint32_t)(A.hs / 8);
             A.level = d;
             A.rem = max_depth - d;
-            A.n = n;
-            A.ev = cur_ev ? cur_ev->as<rr::Event>() : nullptr;
+            A.n = p.cap[d];
+            A.n_dev = d > 0 ? lc + (d - 1) * rr::LC_COUNT + rr::LC_CHILDREN : nullptr;
+            // level d reads ev_b when d is even (d >= 2), ev_a when odd; writes the other one
+            A.ev = d == 0 ? nullptr : (d % 2 ? c->ev_a : c->ev_b).as<rr::Event>();
             A.hit = c->hit.as<rr::HitRec>();
             A.n12 = c->n12.as<double>();
-            A.comb = c->comb[d].as<rr::CombRec>();
+            A.comb = children_possible ? c->comb[d].as<rr::CombRec>() : nullptr;
             A.parent_comb = d > 0 ? c->comb[d - 1].as<rr::CombRec>() : nullptr;
-            A.comb_ext = ext ? c->comb_ext[d].as<rr::CombExt>() : nullptr;
+            A.comb_ext = ext && children_possible ? c->comb_ext[d].as<rr::CombExt>() : nullptr;
             A.parent_ext = ext && d > 0 ? c->comb_ext[d - 1].as<rr::CombExt>() : nullptr;
             A.out = out;
             A.avg = avg;
             A.avg_f32 = avg_f32;
-            A.next = children_possible ? nxt_ev->as<rr::Event>() : nullptr;
-            A.pending = c->pend[d].as<int32_t>();
+            // null when no material is reflective or transparent (or at the last level)
+            A.next = children_possible ? (d % 2 ? c->ev_b : c->ev_a).as<rr::Event>() : nullptr;
+            A.pending = children_possible ? c->pend[d].as<int32_t>() : nullptr;
             A.n1n2_list = c->n1n2.as<int32_t>();
-            A.lcount = c->lcount.as<unsigned int>();
+            A.lcount = lc + d * rr::LC_COUNT;
             A.counters = frame_counters(c, c->epoch);
             A.counters_zero = (c->zero_next && d == 0 && base == 0) ? frame_counters(c, c->epoch ^ 1) : nullptr;
             A.stamps = nullptr;
@@ -241,30 +286,17 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
                 }
             }
 #endif
-            level_n.push_back(n);
-            if (!children_possible) {  // no children at the last level, so nothing is pending
-                level_pend.push_back(0);
-                break;
-            }
-            HIPCHK(hipMemcpyAsync(c->h_lcount, c->lcount.p, rr::LC_COUNT * sizeof(unsigned int), hipMemcpyDeviceToHost,
-                                  st));
-            HIPCHK(hipStreamSynchronize(st));
-            level_pend.push_back((int64_t)c->h_lcount[rr::LC_PENDING]);
-            n = (int64_t)c->h_lcount[rr::LC_CHILDREN];
-            cur_ev = nxt_ev;
-            nxt_ev = (nxt_ev == &c->ev_a) ? &c->ev_b : &c->ev_a;
         }
         // bottom-up shade_hit sums of the events with children (scene.rs:172-177)
-        for (int d = (int)level_n.size() - 1; d >= 0; --d) {
-            if (level_pend[d] == 0) continue;
+        for (int d = p.levels - 2; d >= 0; --d) {
             rr::CombArgs C{};
             C.level = d;
-            C.n = level_pend[d];
+            C.n = p.cap[d];
+            C.n_dev = lc + d * rr::LC_COUNT + rr::LC_PENDING;
             C.base = base;
             C.pending = c->pend[d].as<int32_t>();
             C.comb = c->comb[d].as<rr::CombRec>();
             C.parent_comb = d > 0 ? c->comb[d - 1].as<rr::CombRec>() : nullptr;
-            const bool ext = c->host.has_transparent != 0;
             C.comb_ext = ext ? c->comb_ext[d].as<rr::CombExt>() : nullptr;
             C.parent_ext = ext && d > 0 ? c->comb_ext[d - 1].as<rr::CombExt>() : nullptr;
             C.out = out;
@@ -358,17 +390,19 @@ int rr_create(int device, rr_ctx** out) {
     rr_ctx* c = new rr_ctx();
     c->device = device;
     if (const char* b = std::getenv("RRAY_BATCH")) c->batch = std::max<int64_t>(1024, std::atoll(b));
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) c->queue_budget = free_b / 2;
+    if (const char* q = std::getenv("RRAY_QUEUE_BUDGET_MB")) c->queue_budget = (size_t)std::max(1ll, std::atoll(q)) << 20;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&c->e0);
     if (e == hipSuccess) e = hipEventCreate(&c->e1);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_lcount, 64 * sizeof(unsigned int), hipHostMallocDefault);
     if (e == hipSuccess)
         e = hipHostMalloc((void**)&c->h_counters, kCounterBytes, hipHostMallocDefault);
     if (e == hipSuccess) e = c->counters.ensure(3 * kCounterBytes);
     if (e == hipSuccess) e = hipMemset(c->counters.p, 0, 3 * kCounterBytes);
-    if (e == hipSuccess) e = c->lcount.ensure(64 * sizeof(unsigned int));
+    if (e == hipSuccess) e = c->lcount.ensure((RR_MAX_DEPTH + 1) * rr::LC_COUNT * sizeof(unsigned int));
     if (e != hipSuccess) {
         rr_destroy(c);
         return fail(RR_E_HIP, std::string("context setup: ") + hipGetErrorString(e));
@@ -388,7 +422,6 @@ void rr_destroy(rr_ctx* c) {
     for (auto& b : c->comb_ext) b.release();
     for (auto& b : c->pend) b.release();
     for (hipEvent_t e : c->prof.pool) (void)hipEventDestroy(e);
-    if (c->h_lcount) (void)hipHostFree(c->h_lcount);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->e0) (void)hipEventDestroy(c->e0);
     if (c->e1) (void)hipEventDestroy(c->e1);

@@ -574,6 +574,9 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
         const DevMaterial& m = out.mats[nd.material];
         if (m.transparency != 0.0) out.has_transparent = 1;
         if (m.transparency != 0.0 || m.reflective != 0.0) out.has_secondary = 1;  // scene.rs:281-336
+        // children one shade_hit can queue: reflected (reflective != 0) + refracted (transparency != 0)
+        const int32_t kids = (m.reflective != 0.0 ? 1 : 0) + (m.transparency != 0.0 ? 1 : 0);
+        out.max_children = std::max(out.max_children, kids);
     }
     // culling bounds (parent space) per node
     std::vector<int> obj_of_node(out.nodes.size(), -1);

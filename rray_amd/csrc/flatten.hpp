@@ -23,9 +23,10 @@ struct HostScene {
     std::vector<int32_t> node_of_object;  // object id -> node index (-1 if not in the scene tree)
     int32_t has_transparent = 0;
     int32_t has_secondary = 0;            // some material reflective != 0 or transparency != 0
+    int32_t max_children = 0;             // max secondary rays one shading event queues (0, 1 or 2)
     int32_t has_csg = 0;
     int32_t has_quad = 0;
-    int32_t complex_patterns = 0;         // tree-evaluated patterns (pattern_tree)                 // cubes, cylinders, cones (general kernel variant)
+    int32_t complex_patterns = 0;         // tree-evaluated patterns (pattern_tree)
     int64_t n_top_leaves = 0;             // leaves tested by every ray (reference full scan)
 };
 

@@ -23,7 +23,8 @@ struct LevelArgs {
     int64_t base;            // first local sample of this batch
     const double* rays0;     // level-0 explicit rays (o xyz, d xyz); nullptr: camera rays
     int32_t level, rem;      // level d and `remaining` = max_depth - d
-    int64_t n;               // events at this level
+    int64_t n;               // events at this level (n_dev == null) or this level's capacity (the grid)
+    const unsigned int* n_dev;  // level >= 1: the live event count, written by the previous level's appends
     const Event* ev;         // level >= 1 input queue
     HitRec* hit;
     double* n12;
@@ -47,7 +48,8 @@ struct LevelArgs {
 
 struct CombArgs {
     int32_t level;
-    int64_t n;                 // pending events of this level
+    int64_t n;                 // capacity of this level's pending list (sizes the grid)
+    const unsigned int* n_dev; // the live pending count (LC_PENDING of the level)
     int64_t base;
     const int32_t* pending;
     const CombRec* comb;

@@ -10,6 +10,7 @@
 //   aa_kernel      box average before `as u8`                      canvas.rs:76-96
 // Every kernel is one work-item per queue entry; the node walks inside are wave-uniform (scalar
 // broadcast loads of the flattened scene, culled per wave against the rays' bundle).
+#include <algorithm>
 #include <cstdlib>
 
 #include "device_core.inc"
@@ -175,17 +176,38 @@ __device__ __forceinline__ void block_append(unsigned int* const (&ctr)[NQ], con
     for (int q = 0; q < NQ; ++q) slot[q] = (int32_t)(s_base[q][w] + (unsigned int)__popcll(m[q] & below_mask));
 }
 
+// The live event count of a level.  Levels >= 1 are launched with their worst-case grid (the
+// previous level's capacity x max children, known on the host) and read the real count the previous
+// level's appends produced from HBM, so the host never waits for a level to finish (rray.h:
+// rr_render_device is asynchronous).  Blocks past the count exit at once (block-uniform).
+__device__ __forceinline__ int64_t live_count(const LevelArgs& A) {
+    return A.n_dev ? (int64_t)*A.n_dev : A.n;
+}
+
 enum WalkKind { W_NONE = -1, W_TRACE = 0, W_SHADOW = 1, W_N1N2 = 2 };
-__device__ void flush(Counters& cnt, unsigned long long* counters, int walk = W_NONE) {
-    if ((threadIdx.x & 63) != 0) return;  // every field is wave-uniform
-    counters += (blockIdx.x & (RR_CNT_SLOTS - 1)) * RR_CNT_STRIDE;
-    const uint64_t v[7] = {cnt.rays, cnt.shadow, cnt.shade, cnt.n1n2, cnt.gtests, cnt.ghits, cnt.tests};
-    const int slot[7] = {C_RAYS, C_SHADOW, C_SHADE, C_N1N2, C_GROUP_TESTS, C_GROUP_HITS, C_PRIM_TESTS};
-    for (int k = 0; k < 7; ++k)
-        if (v[k]) atomicAdd(counters + slot[k], (unsigned long long)v[k]);
-    if (walk >= 0) {
-        if (cnt.flops) atomicAdd(counters + C_FLOPS_TRACE + walk, (unsigned long long)cnt.flops);
-        if (cnt.visits) atomicAdd(counters + C_VISITS_TRACE + walk, (unsigned long long)cnt.visits);
+// Counter flush, aggregated per workgroup: the 4 waves' totals are summed in LDS and one thread per
+// counter does a single device-scope atomic (slot = blockIdx % RR_CNT_SLOTS), 4x fewer memory-side
+// atomics than per-wave flushes (they were ~14 % of a C2 frame's HBM writes).  `extra` adds the fused
+// kernels' closest-hit walk flops / visits.  Every thread of the (256-thread) block must call it.
+constexpr int RR_FLUSH_N = 11;
+__device__ void flush(const Counters& cnt, unsigned long long* counters, int walk = W_NONE,
+                      uint64_t trace_flops = 0, uint64_t trace_visits = 0) {
+    __shared__ unsigned long long s_acc[4][RR_FLUSH_N];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) {  // every field is wave-uniform
+        const uint64_t v[RR_FLUSH_N] = {cnt.rays, cnt.shadow, cnt.shade, cnt.n1n2, cnt.gtests, cnt.ghits, cnt.tests,
+                                        walk >= 0 ? (uint64_t)cnt.flops : 0ull, walk >= 0 ? (uint64_t)cnt.visits : 0ull,
+                                        trace_flops, trace_visits};
+        for (int k = 0; k < RR_FLUSH_N; ++k) s_acc[w][k] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < RR_FLUSH_N) {
+        const int k = threadIdx.x;
+        const unsigned long long t = s_acc[0][k] + s_acc[1][k] + s_acc[2][k] + s_acc[3][k];
+        const int slot_of[RR_FLUSH_N] = {C_RAYS, C_SHADOW, C_SHADE, C_N1N2, C_GROUP_TESTS, C_GROUP_HITS, C_PRIM_TESTS,
+                                         C_FLOPS_TRACE + (walk >= 0 ? walk : 0), C_VISITS_TRACE + (walk >= 0 ? walk : 0),
+                                         C_FLOPS_TRACE, C_VISITS_TRACE};
+        if (t) atomicAdd(counters + (blockIdx.x & (RR_CNT_SLOTS - 1)) * RR_CNT_STRIDE + slot_of[k], t);
     }
 }
 
@@ -206,10 +228,12 @@ __device__ __forceinline__ void zero_next_counters(const LevelArgs& A) {
 
 template <int G, bool LC, bool RM>
 __global__ void __launch_bounds__(256) trace_kernel(DevScene S, LevelArgs A) {
+    const int64_t n_live = live_count(A);
+    if ((int64_t)blockIdx.x * blockDim.x >= n_live) return;
     zero_next_counters(A);
     if (LC) stage_culls(S);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool valid = i < A.n;
+    const bool valid = i < n_live;
     Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef RR_STAMPS
     cnt.st = nullptr;
@@ -258,9 +282,10 @@ __global__ void __launch_bounds__(256) trace_kernel(DevScene S, LevelArgs A) {
 
 template <int G, bool LC, bool RM>
 __global__ void __launch_bounds__(256) n1n2_kernel(DevScene S, LevelArgs A) {
+    const int64_t cnt_n = (int64_t)A.lcount[LC_N1N2];
+    if ((int64_t)blockIdx.x * blockDim.x >= cnt_n) return;
     if (LC) stage_culls(S);
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t cnt_n = (int64_t)A.lcount[LC_N1N2];
     const bool valid = j < cnt_n;
     Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int64_t i = valid ? A.n1n2_list[j] : 0;
@@ -454,10 +479,12 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
         }
     }
 #endif
+    const int64_t n_live = live_count(A);
+    if ((int64_t)blockIdx.x * blockDim.x >= n_live) return;
     zero_next_counters(A);
     if (LC) stage_culls(S);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool valid = i < A.n;
+    const bool valid = i < n_live;
     Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t trace_flops = 0;
     uint32_t trace_visits = 0;
@@ -659,19 +686,12 @@ __global__ void __launch_bounds__(256) RR_SHADE_ATTR(PRE, G) shade_kernel(DevSce
         const V3 v = has_hit ? shade_sum(surface, zero, zero, refl, transp, R) : zero;
         deliver(A.level, i, parent, slot, v, A.out, A.avg, A.avg_f32, A.parent_comb, A.parent_ext, ls0);
     }
-    flush(cnt, A.counters, W_SHADOW);
-    if (FUSED && (threadIdx.x & 63) == 0) {
-        unsigned long long* c = A.counters + (blockIdx.x & (RR_CNT_SLOTS - 1)) * RR_CNT_STRIDE;
-        if (trace_flops) atomicAdd(c + C_FLOPS_TRACE, (unsigned long long)trace_flops);
-        if (trace_visits) atomicAdd(c + C_VISITS_TRACE, (unsigned long long)trace_visits);
-    }
+    flush(cnt, A.counters, W_SHADOW, trace_flops, trace_visits);
     RR_STAMP(cnt, 7);
 }
 
 // bottom-up: the pending events of a level, whose children are all finished, complete their sum
-__global__ void __launch_bounds__(256) combine_kernel(CombArgs C) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= C.n) return;
+__device__ __forceinline__ void combine_one(const CombArgs& C, int64_t j) {
     const int64_t i = C.pending[j];
     const CombRec c = C.comb[i];
     V3 b = mk(0.0, 0.0, 0.0);  // no transparency in the scene: refracted_color is black, transparency 0
@@ -688,6 +708,11 @@ __global__ void __launch_bounds__(256) combine_kernel(CombArgs C) {
     const int64_t oi = C.level == 0 ? (C.lrows > 0 ? tile_to_local_u32(t, (uint32_t)C.hs, (uint32_t)C.lrows) : t) : 0;
     deliver(C.level, i, c.parent, (c.flags & CF_REFRACT_CHILD) ? 1 : 0, v, C.out, C.avg, C.avg_f32, C.parent_comb,
             C.parent_ext, oi);
+}
+__global__ void __launch_bounds__(256) combine_kernel(CombArgs C) {
+    const int64_t n = C.n_dev ? (int64_t)*C.n_dev : C.n;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+        combine_one(C, j);
 }
 
 // canvas.rs:85-96: r = 0.0; r += p (dy outer, dx inner); r /= aa*aa
@@ -862,7 +887,9 @@ hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t st, K
 hipError_t launch_combine(const CombArgs& C, hipStream_t st, KernelProf* prof) {
     if (C.n <= 0) return hipSuccess;
     Span s(prof, K_COMBINE, st);
-    hipLaunchKernelGGL(combine_kernel, dim3(blocks_for(C.n)), dim3(256), 0, st, C);
+    // grid-stride over the live count: the capacity can be far above it (worst case per level)
+    const unsigned grid = std::min<unsigned>(blocks_for(C.n), 256u * 16u);
+    hipLaunchKernelGGL(combine_kernel, dim3(grid), dim3(256), 0, st, C);
     return hipGetLastError();
 }
 
