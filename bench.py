@@ -116,6 +116,10 @@ def main():
     ap.add_argument("--kernel-events", choices=("separate", "timed"), default="separate",
                     help="per-launch HIP events for the roofline: over a second pass of K steps (default) or "
                          "inside the timed region")
+    ap.add_argument("--gather", choices=("abi", "torch"), default="abi",
+                    help="tiles at N>1: the library's own RCCL group (rr_create_rank + rr_render_gather_device; the "
+                         "torch process group only carries host-side coordination over gloo) or torch.distributed's "
+                         "RCCL gather of the tiles (rray_amd/dist.py FramePipeline)")
     ap.add_argument("--force-dist", action="store_true",
                     help="rehearsal: run the multi-rank path (RCCL process group, pipelined gather) even at 1 rank")
     ap.add_argument("--dry-run", action="store_true",
@@ -138,7 +142,7 @@ class Session:
     """One workload on this rank: the scene in HBM and a `step()` that renders one frame (frames mode /
     one part) or this rank's tile of one frame plus the pipelined gather (tiles mode)."""
 
-    def __init__(self, R, workload, dev, local, rank, world, tiles, distributed, rend):
+    def __init__(self, R, workload, dev, local, rank, world, tiles, distributed, rend, gather="abi"):
         import torch
         from rray_amd import dist as rdist
 
@@ -153,14 +157,26 @@ class Session:
         self.dev = dev
         self.tiles = tiles
         self.multi = distributed and tiles
+        self.gather = gather
+        self.rank = rank
         self.pipe = None
         self.tile = None
+        self.frame_t = None
         part, nparts = (rank, world) if tiles else (0, 1)
         rows = R.part_rows(self.H, part, nparts, BLOCK)
         if not self.multi:
             # the AA-averaged f64 image (the drop-in's Canvas, before `as u8`)
             self.tile = torch.zeros((len(rows), self.W, 3), dtype=torch.float64, device=dev)
             self.opts = R._lib.RenderOpts(self.aa, self.depth, 0, 0, part, nparts, BLOCK,
+                                          R._lib.RR_OUT_AVG | R._lib.RR_NO_FRAME_TIMING)
+            self.stream = torch.cuda.current_stream(dev)
+        elif gather == "abi":
+            # the library's group context splits the frame into this rank's row tile, gathers the f64
+            # tiles to rank 0 with one RCCL gather (double-buffered: frame k+1 renders while frame k is
+            # gathered) and un-interleaves them into frame_t
+            if rank == 0:
+                self.frame_t = torch.zeros((self.H, self.W, 3), dtype=torch.float64, device=dev)
+            self.opts = R._lib.RenderOpts(self.aa, self.depth, 0, 0, 0, 1, BLOCK,
                                           R._lib.RR_OUT_AVG | R._lib.RR_NO_FRAME_TIMING)
             self.stream = torch.cuda.current_stream(dev)
         else:
@@ -177,6 +193,10 @@ class Session:
         if not self.multi:
             self.rend.render_device(self.cam, self.opts, None, self.tile.data_ptr(), self.stream.cuda_stream)
             return
+        if self.gather == "abi":
+            self.rend.render_gather_device(self.cam, self.opts, self.frame_t.data_ptr() if self.rank == 0 else None,
+                                           self.stream.cuda_stream)
+            return
         i, buf, prev = self.pipe.acquire()
         with torch.cuda.stream(self.stream):
             if prev is not None:
@@ -187,6 +207,8 @@ class Session:
 
     def frame(self):
         """The latest assembled AA-averaged frame (rank 0 in tiles mode), as a CPU numpy array."""
+        if self.multi and self.gather == "abi":
+            return self.frame_t.cpu().numpy() if self.frame_t is not None else None
         if self.multi:
             return self.pipe.frame.cpu().numpy() if self.pipe.frame is not None else None
         return self.tile.cpu().numpy()
@@ -194,7 +216,7 @@ class Session:
 
 def timed_loop(sess, steps, warmup, distributed, dist, torch, kernel_events="separate"):
     def sync():
-        if sess.multi:
+        if sess.pipe is not None:
             sess.pipe.drain()
         torch.cuda.synchronize(sess.dev)
         if distributed:
@@ -224,7 +246,9 @@ def timed_loop(sess, steps, warmup, distributed, dist, torch, kernel_events="sep
     stats = sess.rend.last_stats()
     elapsed = t1 - t0
     if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=sess.dev)
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        if dist.get_backend() == "nccl":
+            t = t.to(sess.dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed, (t_enq - t0), ktimes, stats, in_region
@@ -336,14 +360,30 @@ def gpu_bench(args, world, mode, workload):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     distributed = world > 1 or args.force_dist
-    if distributed:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     tiles = mode == "tiles"
+    abi_group = distributed and tiles and args.gather == "abi"
+    if distributed and "RANK" not in os.environ:  # --force-dist outside torchrun: a 1-rank group
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(sk.getsockname()[1]))
+        sk.close()
+    if distributed:
+        if abi_group:  # RCCL lives in the library; the process group only coordinates the hosts
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import rray_amd as R
 
     dev = torch.device("cuda", local)
-    rend = R.Renderer(local)
-    sess = Session(R, workload, dev, local, rank, world, tiles, distributed, rend)
+    torch.zeros(1, device=dev)  # torch's HIP runtime initialises first (the library shares it)
+    if abi_group:
+        uid = [R.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        rend = R.Renderer.rank(local, world, rank, uid[0])
+    else:
+        rend = R.Renderer(local)
+    sess = Session(R, workload, dev, local, rank, world, tiles, distributed, rend, args.gather)
     big = WORKLOADS[workload][1] * WORKLOADS[workload][2] * WORKLOADS[workload][3] ** 2 > 20_000_000
     steps = args.steps if args.steps is not None else (10 if big else 50)
     warmup = args.warmup if args.warmup is not None else (2 if big else 10)
@@ -359,7 +399,10 @@ def gpu_bench(args, world, mode, workload):
     if sess.multi:
         gathered = sess.frame() if rank == 0 else None
         if rank == 0:
-            full = rend.render(sess.cam, aa=sess.aa, max_depth=sess.depth)["avg"]
+            one = R.Renderer(local)  # a plain single-device context renders the whole frame as one part
+            one.upload(sess.scene)
+            full = one.render(sess.cam, aa=sess.aa, max_depth=sess.depth)["avg"]
+            one.close()
             identity = {"bit_identical_to_1_part": bool(np.array_equal(gathered, full)),
                         "max_abs_diff": float(np.max(np.abs(gathered - full)))}
         dist.barrier()
@@ -377,7 +420,9 @@ def gpu_bench(args, world, mode, workload):
                       "ms_per_step": round(a_el / 5 * 1e3, 4), "steps": 5, "warmup": 1,
                       "note": "N=1 value of the N>1 workload (row tiles with nparts=1), for the scaling curve"}
     if rank == 0:
-        par = (f"row-tiles x{world} + rccl gather (f64 tiles, pipelined)" if world > 1 or sess.multi else
+        via = ("library RCCL group: rr_create_rank + rr_render_gather_device" if args.gather == "abi" else
+               "torch.distributed RCCL gather")
+        par = (f"row-tiles x{world} + rccl gather (f64 tiles, pipelined; {via})" if world > 1 or sess.multi else
                "single GPU, whole frame") if tiles else \
             f"frame-parallel x{world} (one whole frame per rank per step, no data-path collective)"
         line = {"metric": METRIC, "value": round(value, 3), "unit": "Mpixel-samples/s", "n_gpus": world,

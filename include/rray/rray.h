@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 4
+#define RR_ABI_VERSION 5
 
 /* error codes */
 #define RR_OK 0
@@ -158,8 +158,34 @@ int rr_device_count(int* out);
 /* ---- context: one device, one stream (not thread-safe; one render at a time) ---- */
 int rr_create(int device, rr_ctx** out);
 void rr_destroy(rr_ctx* ctx);
-/* flattens (DFS order, 3x4 inverses, group AABBs) and uploads to HBM (scene.rs, group.rs) */
+/* flattens (DFS order, 3x4 inverses, group AABBs) and uploads to HBM (scene.rs, group.rs);
+ * a multi-device context replicates the scene to every device */
 int rr_scene_upload(rr_ctx* ctx, const rr_scene_desc* desc);
+
+/* ---- multi-device contexts (ABI 5): one frame across several GPUs (camera.rs:107-121 spreads one
+ * frame over every rayon worker).  Global rank r renders the output rows {y : (y/block_rows) % N == r}
+ * as an f64 AA-averaged tile; one RCCL gather (ncclGather over xGMI) brings the tiles to rank 0,
+ * which un-interleaves them into frame order.  The context owns a render and a gather stream per
+ * device and the RCCL communicator.  rr_render (blocking; out_avg filled on rank 0 only) and
+ * rr_render_gather_device (asynchronous) take part 0 of 1: the context does the split.  Only the
+ * f64 averaged image is produced (no RR_OUT_CANVAS / RR_OUT_AVG_F32).  rr_color_at / rr_is_shadowed /
+ * rr_kernel_times act on the context's first local device; rr_last_stats sums its local devices. */
+#define RR_RCCL_ID_BYTES 128
+/* this process drives n devices (ncclCommInitAll); images are bit-identical to one device's */
+int rr_create_multi(int n_devices, const int* device_ids, rr_ctx** out);
+/* one process per GPU: rank 0 makes an id with rr_rccl_unique_id, the host shares it (any channel),
+ * every rank calls rr_create_rank with it (ncclCommInitRank; collective) */
+int rr_rccl_unique_id(uint8_t* out, int32_t n_bytes);
+int rr_create_rank(int device, int nranks, int rank, const uint8_t* unique_id, rr_ctx** out);
+/* nranks in the group, this context's first global rank, devices this context drives (1/0/1 for rr_create) */
+int rr_context_info(const rr_ctx* ctx, int32_t* nranks, int32_t* rank, int32_t* ndevices);
+/* Whole frame -> d_frame (W*H*3 doubles on rank 0's device; ignored on other ranks), enqueued after
+ * the work already on `hip_stream` (NULL: no ordering with the caller) and completed in its order;
+ * not synchronised.  Collective: every rank calls it for every frame.  Tiles are double-buffered, so
+ * frame k+1 renders while frame k is being gathered.  On a single-device context it is
+ * rr_render_device(d_avg = d_frame). */
+int rr_render_gather_device(rr_ctx* ctx, const rr_camera* cam, const rr_render_opts* opts, void* d_frame,
+                            void* hip_stream);
 
 /* Camera::new (camera.rs:41-63) */
 int rr_camera_new(int64_t hsize, int64_t vsize, double field_of_view, const double transform[16], rr_camera* out);
@@ -212,6 +238,9 @@ int rr_write_png(const char* path, const uint8_t* rgba, int64_t width, int64_t h
 /* render_scene_from_file (scene_builder_yaml.rs:429-436) on `device` */
 int rr_render_scene_from_file(const char* path, int64_t width, int64_t height, const char* png_file, int32_t aa,
                               int device);
+/* the same on n devices of this process (rr_create_multi) */
+int rr_render_scene_from_file_devices(const char* path, int64_t width, int64_t height, const char* png_file,
+                                      int32_t aa, int n_devices, const int* device_ids);
 
 #ifdef __cplusplus
 }

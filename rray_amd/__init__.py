@@ -14,10 +14,11 @@ from .render import (  # noqa: F401
     device_count,
     part_rows,
     quantize,
+    rccl_unique_id,
     render_scene_from_file,
     render_scene_from_str,
     write_png,
 )
 
 __all__ = ["Renderer", "SceneBuilder", "YamlScene", "camera", "part_rows", "quantize", "write_png",
-           "render_scene_from_str", "render_scene_from_file", "device_count", "RRError", "lib"]
+           "render_scene_from_str", "render_scene_from_file", "device_count", "rccl_unique_id", "RRError", "lib"]

@@ -68,7 +68,9 @@ EXPORTS = ["rr_abi_version", "rr_last_error", "rr_device_count", "rr_create", "r
            "rr_camera_new", "rr_render", "rr_render_device", "rr_part_rows", "rr_kernel_profile", "rr_kernel_times",
            "rr_last_stats", "rr_color_at",
            "rr_is_shadowed", "rr_scene_inspect", "rr_scene_from_yaml", "rr_scene_desc_of", "rr_scene_free", "rr_quantize",
-           "rr_write_png", "rr_render_scene_from_file"]
+           "rr_write_png", "rr_render_scene_from_file", "rr_render_scene_from_file_devices", "rr_create_multi",
+           "rr_rccl_unique_id", "rr_create_rank", "rr_context_info", "rr_render_gather_device"]
+RCCL_ID_BYTES = 128
 
 _lib = None
 
@@ -113,6 +115,14 @@ def lib():
     L.rr_quantize.argtypes = [_D, C.c_int64, C.POINTER(C.c_uint8)]
     L.rr_write_png.argtypes = [C.c_char_p, C.POINTER(C.c_uint8), C.c_int64, C.c_int64]
     L.rr_render_scene_from_file.argtypes = [C.c_char_p, C.c_int64, C.c_int64, C.c_char_p, C.c_int32, C.c_int]
+    L.rr_render_scene_from_file_devices.argtypes = [C.c_char_p, C.c_int64, C.c_int64, C.c_char_p, C.c_int32, C.c_int,
+                                                    C.POINTER(C.c_int)]
+    L.rr_create_multi.argtypes = [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_void_p)]
+    L.rr_rccl_unique_id.argtypes = [C.POINTER(C.c_uint8), C.c_int32]
+    L.rr_create_rank.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.POINTER(C.c_void_p)]
+    L.rr_context_info.argtypes = [C.c_void_p, _I, _I, _I]
+    L.rr_render_gather_device.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(RenderOpts), C.c_void_p,
+                                          C.c_void_p]
     _lib = L
     return L
 

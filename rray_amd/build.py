@@ -23,7 +23,7 @@ ARCH = "gfx950"
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
           "-I" + os.path.join(ROOT, "include")]
 DEVICE = ["--offload-arch=" + ARCH, "-mllvm", "-disable-promote-alloca-to-lds"]
-SOURCES = ["render.hip", "api.cpp", "flatten.cpp", "frontend.cpp", "yaml.cpp", "png.cpp"]
+SOURCES = ["render.hip", "api.cpp", "multi.cpp", "flatten.cpp", "frontend.cpp", "yaml.cpp", "png.cpp"]
 
 
 def _deps_mtime():
@@ -84,7 +84,7 @@ def build(verbose=False, jobs=None):
         objs = list(ex.map(lambda s: _compile(s, dm, verbose), SOURCES))
     newest = max(os.path.getmtime(o) for o in objs)
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
-        cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", LIB] + objs + ["-lz", "-Wl,-soname,librray_amd.so"]
+        cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", LIB] + objs + ["-lz", "-L/opt/rocm/lib", "-lrccl", "-Wl,-soname,librray_amd.so"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")

@@ -12,6 +12,7 @@
 #include "../../include/rray/rray.h"
 #include "flatten.hpp"
 #include "kernels.hpp"
+#include "multi.hpp"
 #include "rr_math.hpp"
 
 namespace {
@@ -59,6 +60,7 @@ struct DBuf {
 void rr_set_error(const char* msg) { g_err = msg ? msg : ""; }
 
 struct rr_ctx {
+    rr_group* group = nullptr;  // multi-device context (multi.cpp): everything below is unused
     int device = 0;
     hipStream_t stream = nullptr;
     bool has_scene = false;
@@ -411,8 +413,46 @@ int rr_create(int device, rr_ctx** out) {
     return RR_OK;
 }
 
+int rr_create_multi(int n, const int* device_ids, rr_ctx** out) {
+    if (!out) return fail(RR_E_ARG, "null out");
+    *out = nullptr;
+    rr_group* g = nullptr;
+    int rc = rr::group_create_local(n, device_ids, &g);
+    if (rc != RR_OK) return rc;
+    rr_ctx* c = new rr_ctx();
+    c->group = g;
+    *out = c;
+    return RR_OK;
+}
+
+int rr_create_rank(int device, int nranks, int rank, const uint8_t* unique_id, rr_ctx** out) {
+    if (!out) return fail(RR_E_ARG, "null out");
+    *out = nullptr;
+    rr_group* g = nullptr;
+    int rc = rr::group_create_rank(device, nranks, rank, unique_id, &g);
+    if (rc != RR_OK) return rc;
+    rr_ctx* c = new rr_ctx();
+    c->group = g;
+    *out = c;
+    return RR_OK;
+}
+
+int rr_context_info(const rr_ctx* c, int32_t* nranks, int32_t* rank, int32_t* ndevices) {
+    if (!c) return fail(RR_E_ARG, "null context");
+    if (c->group) return rr::group_info(c->group, nranks, rank, ndevices);
+    if (nranks) *nranks = 1;
+    if (rank) *rank = 0;
+    if (ndevices) *ndevices = 1;
+    return RR_OK;
+}
+
 void rr_destroy(rr_ctx* c) {
     if (!c) return;
+    if (c->group) {
+        rr::group_destroy(c->group);
+        delete c;
+        return;
+    }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)sync_ctx(c);
     for (DBuf* b : {&c->culls, &c->chunks, &c->nodes, &c->groups, &c->shapes, &c->tris, &c->mats, &c->pats, &c->lights, &c->textures, &c->texels, &c->counters,
@@ -433,6 +473,7 @@ void rr_destroy(rr_ctx* c) {
 
 int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     if (!c || !d) return fail(RR_E_ARG, "null context/descriptor");
+    if (c->group) return rr::group_upload(c->group, d);
     std::string err;
     rr::HostScene hs;
     int rc = rr::flatten_scene(*d, hs, err);
@@ -546,6 +587,7 @@ int64_t rr_part_rows(int64_t height, int32_t part, int32_t nparts, int32_t block
 int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, void* d_canvas, void* d_avg,
                      void* hip_stream) {
     if (!c) return fail(RR_E_ARG, "null context");
+    if (c->group) return fail(RR_E_ARG, "multi-device context: use rr_render_gather_device or rr_render");
     if (!c->has_scene) return fail(RR_E_ARG, "no scene uploaded");
     int rc = check_opts(cam, o);
     if (rc != RR_OK) return rc;
@@ -603,8 +645,19 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     return RR_OK;
 }
 
+int rr_render_gather_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, void* d_frame, void* hip_stream) {
+    if (!c) return fail(RR_E_ARG, "null context");
+    if (c->group) return rr::group_render_gather(c->group, cam, o, d_frame, hip_stream);
+    if (o && (o->nparts != 1 || o->part != 0)) return fail(RR_E_ARG, "rr_render_gather_device renders the whole frame");
+    if (o && (o->flags & (RR_OUT_CANVAS | RR_OUT_AVG_F32)))
+        return fail(RR_E_ARG, "rr_render_gather_device writes the f64 AA-averaged image only");
+    if (!d_frame) return fail(RR_E_ARG, "null frame buffer");
+    return rr_render_device(c, cam, o, nullptr, d_frame, hip_stream);
+}
+
 int rr_kernel_profile(rr_ctx* c, int enable) {
     if (!c) return fail(RR_E_ARG, "null context");
+    if (c->group) return rr_kernel_profile(rr::group_local(c->group, 0), enable);
     HIPCHK(sync_ctx(c));
     int rc = resolve_prof(c);
     if (rc != RR_OK) return rc;
@@ -618,6 +671,7 @@ int rr_kernel_profile(rr_ctx* c, int enable) {
 
 int rr_kernel_times(rr_ctx* c, double* ms, uint64_t* launches, int32_t n) {
     if (!c) return fail(RR_E_ARG, "null context");
+    if (c->group) return rr_kernel_times(rr::group_local(c->group, 0), ms, launches, n);
     HIPCHK(sync_ctx(c));
     int rc = resolve_prof(c);
     if (rc != RR_OK) return rc;
@@ -630,6 +684,7 @@ int rr_kernel_times(rr_ctx* c, double* ms, uint64_t* launches, int32_t n) {
 
 int rr_last_stats(rr_ctx* c, rr_stats* s) {
     if (!c || !s) return fail(RR_E_ARG, "null argument");
+    if (c->group) return rr::group_last_stats(c->group, s);
     uint64_t samples = c->last.samples;
     int rc = finish_stats(c);
     if (rc != RR_OK) return rc;
@@ -641,6 +696,7 @@ int rr_last_stats(rr_ctx* c, rr_stats* s) {
 int rr_render(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, double* out_canvas, double* out_avg,
               rr_stats* stats) {
     if (!c) return fail(RR_E_ARG, "null context");
+    if (c->group) return rr::group_render(c->group, cam, o, out_canvas, out_avg, stats);
     int rc = check_opts(cam, o);
     if (rc != RR_OK) return rc;
     const int32_t block = o->block_rows > 0 ? o->block_rows : 8;
@@ -665,6 +721,7 @@ int rr_render(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, double* 
 
 int rr_color_at(rr_ctx* c, int64_t n, const double* origins, const double* directions, int32_t remaining,
                 uint64_t seed, int32_t jitter_mode, double* out_rgb) {
+    if (c && c->group) return rr_color_at(rr::group_local(c->group, 0), n, origins, directions, remaining, seed, jitter_mode, out_rgb);
     if (!c || (n > 0 && (!origins || !directions || !out_rgb))) return fail(RR_E_ARG, "null argument");
     if (!c->has_scene) return fail(RR_E_ARG, "no scene uploaded");
     if (remaining < 0 || remaining > RR_MAX_DEPTH) return fail(RR_E_LIMIT, "remaining out of range");
@@ -701,6 +758,7 @@ int rr_color_at(rr_ctx* c, int64_t n, const double* origins, const double* direc
 }
 
 int rr_is_shadowed(rr_ctx* c, int64_t n, const double* points, const double* light_positions, int32_t* out) {
+    if (c && c->group) return rr_is_shadowed(rr::group_local(c->group, 0), n, points, light_positions, out);
     if (!c || (n > 0 && (!points || !light_positions || !out))) return fail(RR_E_ARG, "null argument");
     if (!c->has_scene) return fail(RR_E_ARG, "no scene uploaded");
     if (n == 0) return RR_OK;

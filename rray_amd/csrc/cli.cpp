@@ -1,10 +1,13 @@
 // cli.cpp — `rray` drop-in CLI (src/main.rs:49-77): same flags and defaults.
 //   rray -W <width=800> -H <height=600> -s <scene.yaml> -o <output.png> -a <aa=1, max 5>
-// Renders on GPU 0 (RRAY_DEVICE overrides); no CPU fallback.
+// Renders on GPU 0 (RRAY_DEVICE=<id> picks another one); RRAY_DEVICES=<id,id,...> or RRAY_DEVICES=all
+// splits the frame over several GPUs of this host (rr_create_multi: row tiles + one RCCL gather).
+// No CPU fallback.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/rray/rray.h"
 
@@ -60,8 +63,31 @@ int main(int argc, char** argv) {
     }
     if (scene.empty()) return usage("the following required arguments were not provided: --scene <SCENE>");
     if (width <= 0 || height <= 0 || aa <= 0) return usage("width, height and aa must be >= 1");
-    int device = std::getenv("RRAY_DEVICE") ? std::atoi(std::getenv("RRAY_DEVICE")) : 0;
-    int rc = rr_render_scene_from_file(scene.c_str(), width, height, output.c_str(), (int)aa, device);
+    std::vector<int> devices;
+    if (const char* ds = std::getenv("RRAY_DEVICES")) {
+        if (std::strcmp(ds, "all") == 0) {
+            int n = 0;
+            rr_device_count(&n);
+            for (int i = 0; i < n; ++i) devices.push_back(i);
+        } else {
+            for (const char* p = ds; *p;) {
+                char* end = nullptr;
+                long v = std::strtol(p, &end, 10);
+                if (end == p || v < 0) return usage("RRAY_DEVICES must be `all` or a comma-separated list of ids");
+                devices.push_back((int)v);
+                p = *end == ',' ? end + 1 : end;
+                if (*end && *end != ',') return usage("RRAY_DEVICES must be `all` or a comma-separated list of ids");
+            }
+        }
+        if (devices.empty()) {
+            std::fprintf(stderr, "rray: no GPU device available\n");
+            return 1;
+        }
+    } else {
+        devices.push_back(std::getenv("RRAY_DEVICE") ? std::atoi(std::getenv("RRAY_DEVICE")) : 0);
+    }
+    int rc = rr_render_scene_from_file_devices(scene.c_str(), width, height, output.c_str(), (int)aa,
+                                               (int)devices.size(), devices.data());
     if (rc != RR_OK) {
         std::fprintf(stderr, "rray: %s (code %d)\n", rr_last_error(), rc);
         return 1;

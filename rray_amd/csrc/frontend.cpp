@@ -557,6 +557,15 @@ int rr_write_png(const char* path, const uint8_t* rgba, int64_t w, int64_t h) {
 
 int rr_render_scene_from_file(const char* path, int64_t width, int64_t height, const char* png_file, int32_t aa,
                               int device) {
+    return rr_render_scene_from_file_devices(path, width, height, png_file, aa, 1, &device);
+}
+
+int rr_render_scene_from_file_devices(const char* path, int64_t width, int64_t height, const char* png_file,
+                                      int32_t aa, int n_devices, const int* device_ids) {
+    if (n_devices < 1 || !device_ids) {
+        rr_set_error("need at least one device");
+        return RR_E_ARG;
+    }
     std::ifstream f(path ? path : "", std::ios::binary);
     if (!path || !f) {  // scene_builder_yaml.rs:434 panics "File does not exist"
         rr_set_error("File does not exist");
@@ -569,7 +578,7 @@ int rr_render_scene_from_file(const char* path, int64_t width, int64_t height, c
     int rc = rr_scene_from_yaml(ss.str().c_str(), nullptr, width, height, aa, &S, &cam);
     if (rc != RR_OK) return rc;
     rr_ctx* ctx = nullptr;
-    rc = rr_create(device, &ctx);
+    rc = n_devices == 1 ? rr_create(device_ids[0], &ctx) : rr_create_multi(n_devices, device_ids, &ctx);
     if (rc == RR_OK) rc = rr_scene_upload(ctx, rr_scene_desc_of(S));
     std::vector<double> avg((size_t)width * height * 3);
     if (rc == RR_OK) {

@@ -1,0 +1,373 @@
+// multi.cpp — multi-device render contexts: row-interleaved tiles + one RCCL gather.
+//
+// Camera::render (camera.rs:107-121) spreads one frame over every rayon worker; here one frame is
+// spread over GPUs.  Global rank r renders the output rows {y : (y / block) % nranks == r} (the
+// interleaving balances sky and floor cost) as an f64 AA-averaged tile in its own HBM, padded to
+// the largest part's row count; one ncclGather (RCCL over xGMI) brings the tiles to rank 0, whose
+// own tile is rendered in place into the gather buffer, and a small kernel un-interleaves them into
+// frame order.  Two tile buffers alternate so that rendering frame k+1 overlaps the gather of frame
+// k: a render waits only for the gather that last read its buffer.
+//
+// Two shapes of the same group: rr_create_multi (this process drives n devices, ncclCommInitAll,
+// ncclGroupStart/End around the per-device gathers) and rr_create_rank (one process per GPU,
+// ncclCommInitRank from an id made by rr_rccl_unique_id on rank 0 and shared by the host).
+#include "multi.hpp"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+
+void rr_set_error(const char* msg);  // api.cpp
+
+namespace {
+
+int gfail(int code, const std::string& msg) {
+    rr_set_error(msg.c_str());
+    return code;
+}
+#define GHIP(expr)                                                                              \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess) return gfail(RR_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+#define GNCCL(expr)                                                                             \
+    do {                                                                                        \
+        ncclResult_t r_ = (expr);                                                               \
+        if (r_ != ncclSuccess) return gfail(RR_E_HIP, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+struct DevMem {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, std::max<size_t>(want, 256));
+        if (e == hipSuccess) bytes = std::max<size_t>(want, 256);
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+int64_t rows_of(int64_t height, int32_t part, int32_t nparts, int32_t block) {
+    int64_t n = 0;
+    for (int64_t b0 = (int64_t)part * block; b0 < height; b0 += (int64_t)nparts * block)
+        n += std::min<int64_t>(block, height - b0);
+    return n;
+}
+
+// Gathered tiles -> frame order: output row y belongs to part p = (y / block) % nparts, where it is
+// local row j = (y / (block * nparts)) * block + y % block of p's padded tile.  One thread per double;
+// both sides are contiguous along a row.
+__global__ void __launch_bounds__(256) unshuffle_kernel(const double* __restrict__ in, double* __restrict__ out,
+                                                        int64_t row_len, int64_t height, int32_t nparts, int32_t block,
+                                                        int64_t max_rows) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= row_len * height) return;
+    const int64_t y = i / row_len, x = i - y * row_len;
+    const int64_t p = (y / block) % nparts, j = (y / ((int64_t)block * nparts)) * block + y % block;
+    out[i] = in[(p * max_rows + j) * row_len + x];
+}
+
+hipError_t launch_unshuffle(const double* in, double* out, int64_t W, int64_t H, int32_t nparts, int32_t block,
+                            int64_t max_rows, hipStream_t st) {
+    const int64_t n = W * 3 * H;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(unshuffle_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, out, W * 3, H,
+                       nparts, block, max_rows);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+struct rr_group {
+    int nranks = 1, rank0 = 0;
+    std::vector<int> devices;
+    std::vector<rr_ctx*> subs;
+    std::vector<ncclComm_t> comms;
+    std::vector<hipStream_t> render_st, comm_st;
+    std::vector<hipEvent_t> ev_rendered[2], ev_gathered[2];
+    hipEvent_t ev_caller = nullptr;       // root: the caller's stream position at the gather call
+    std::vector<DevMem> tile[2];          // non-root local devices: their tile; root: unused
+    DevMem recv[2];                       // root: nranks x padded tile (slot 0 = its own tile, in place)
+    DevMem frame;                         // root: assembled frame for the blocking rr_render
+    int64_t k = 0;                        // frames issued (buffer = k % 2)
+    bool root_here() const { return rank0 == 0; }
+};
+
+namespace rr {
+
+static int group_setup(rr_group* g) {
+    const int n = (int)g->devices.size();
+    g->subs.assign(n, nullptr);
+    g->render_st.assign(n, nullptr);
+    g->comm_st.assign(n, nullptr);
+    for (int b = 0; b < 2; ++b) {
+        g->ev_rendered[b].assign(n, nullptr);
+        g->ev_gathered[b].assign(n, nullptr);
+        g->tile[b].resize(n);
+    }
+    for (int l = 0; l < n; ++l) {
+        int rc = rr_create(g->devices[l], &g->subs[l]);
+        if (rc != RR_OK) return rc;
+        GHIP(hipSetDevice(g->devices[l]));
+        GHIP(hipStreamCreateWithFlags(&g->render_st[l], hipStreamNonBlocking));
+        GHIP(hipStreamCreateWithFlags(&g->comm_st[l], hipStreamNonBlocking));
+        for (int b = 0; b < 2; ++b) {
+            GHIP(hipEventCreateWithFlags(&g->ev_rendered[b][l], hipEventDisableTiming));
+            GHIP(hipEventCreateWithFlags(&g->ev_gathered[b][l], hipEventDisableTiming));
+        }
+    }
+    if (g->root_here()) {
+        GHIP(hipSetDevice(g->devices[0]));
+        GHIP(hipEventCreateWithFlags(&g->ev_caller, hipEventDisableTiming));
+    }
+    return RR_OK;
+}
+
+int group_create_local(int n, const int* ids, rr_group** out) {
+    if (!out || n < 1 || !ids) return gfail(RR_E_ARG, "rr_create_multi: need n >= 1 device ids");
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return gfail(RR_E_HIP, "no HIP device available");
+    for (int i = 0; i < n; ++i) {
+        if (ids[i] < 0 || ids[i] >= count) return gfail(RR_E_ARG, "device index out of range");
+        for (int j = 0; j < i; ++j)
+            if (ids[j] == ids[i]) return gfail(RR_E_ARG, "rr_create_multi: device ids must be distinct");
+    }
+    rr_group* g = new rr_group();
+    g->nranks = n;
+    g->rank0 = 0;
+    g->devices.assign(ids, ids + n);
+    int rc = group_setup(g);
+    if (rc == RR_OK) {
+        g->comms.assign(n, nullptr);
+        ncclResult_t r = ncclCommInitAll(g->comms.data(), n, ids);
+        if (r != ncclSuccess) {
+            g->comms.clear();
+            rc = gfail(RR_E_HIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+        }
+    }
+    if (rc != RR_OK) {
+        std::string msg = rr_last_error();
+        group_destroy(g);
+        return gfail(rc, msg);
+    }
+    *out = g;
+    return RR_OK;
+}
+
+int group_create_rank(int device, int nranks, int rank, const uint8_t* unique_id, rr_group** out) {
+    if (!out || nranks < 1 || rank < 0 || rank >= nranks || !unique_id)
+        return gfail(RR_E_ARG, "rr_create_rank: need 0 <= rank < nranks and an RCCL unique id");
+    *out = nullptr;
+    rr_group* g = new rr_group();
+    g->nranks = nranks;
+    g->rank0 = rank;
+    g->devices.assign(1, device);
+    int rc = group_setup(g);
+    if (rc == RR_OK) {
+        ncclUniqueId id;
+        std::memcpy(&id, unique_id, sizeof(id));
+        g->comms.assign(1, nullptr);
+        (void)hipSetDevice(device);
+        ncclResult_t r = ncclCommInitRank(&g->comms[0], nranks, id, rank);
+        if (r != ncclSuccess) {
+            g->comms.clear();
+            rc = gfail(RR_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        }
+    }
+    if (rc != RR_OK) {
+        std::string msg = rr_last_error();
+        group_destroy(g);
+        return gfail(rc, msg);
+    }
+    *out = g;
+    return RR_OK;
+}
+
+void group_destroy(rr_group* g) {
+    if (!g) return;
+    for (size_t l = 0; l < g->devices.size(); ++l) {
+        (void)hipSetDevice(g->devices[l]);
+        if (l < g->render_st.size() && g->render_st[l]) (void)hipStreamSynchronize(g->render_st[l]);
+        if (l < g->comm_st.size() && g->comm_st[l]) (void)hipStreamSynchronize(g->comm_st[l]);
+    }
+    for (ncclComm_t c : g->comms)
+        if (c) (void)ncclCommDestroy(c);
+    for (size_t l = 0; l < g->devices.size(); ++l) {
+        (void)hipSetDevice(g->devices[l]);
+        for (int b = 0; b < 2; ++b) {
+            if (l < g->tile[b].size()) g->tile[b][l].release();
+            if (l < g->ev_rendered[b].size() && g->ev_rendered[b][l]) (void)hipEventDestroy(g->ev_rendered[b][l]);
+            if (l < g->ev_gathered[b].size() && g->ev_gathered[b][l]) (void)hipEventDestroy(g->ev_gathered[b][l]);
+        }
+        if (l < g->render_st.size() && g->render_st[l]) (void)hipStreamDestroy(g->render_st[l]);
+        if (l < g->comm_st.size() && g->comm_st[l]) (void)hipStreamDestroy(g->comm_st[l]);
+        if (l == 0 && g->root_here()) {
+            for (int b = 0; b < 2; ++b) g->recv[b].release();
+            g->frame.release();
+            if (g->ev_caller) (void)hipEventDestroy(g->ev_caller);
+        }
+    }
+    for (rr_ctx* s : g->subs)
+        if (s) rr_destroy(s);
+    delete g;
+}
+
+int group_upload(rr_group* g, const rr_scene_desc* d) {
+    for (size_t l = 0; l < g->subs.size(); ++l) {  // the scene is replicated to every device (<= a few MB)
+        GHIP(hipSetDevice(g->devices[l]));
+        GHIP(hipStreamSynchronize(g->render_st[l]));
+        GHIP(hipStreamSynchronize(g->comm_st[l]));
+        int rc = rr_scene_upload(g->subs[l], d);
+        if (rc != RR_OK) return rc;
+    }
+    return RR_OK;
+}
+
+int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts* o, void* d_frame, void* stream) {
+    if (!cam || !o) return gfail(RR_E_ARG, "null camera/options");
+    if (o->nparts != 1 || o->part != 0)
+        return gfail(RR_E_ARG, "a multi-device context splits the whole frame itself: pass part 0 of 1");
+    if (o->flags & (RR_OUT_CANVAS | RR_OUT_AVG_F32))
+        return gfail(RR_E_ARG, "multi-device contexts produce the f64 AA-averaged image only (RR_OUT_AVG)");
+    if (o->aa < 1 || cam->hsize <= 0 || cam->vsize <= 0 || cam->hsize % o->aa || cam->vsize % o->aa)
+        return gfail(RR_E_ARG, "camera size must be a positive multiple of aa");
+    if (g->root_here() && !d_frame) return gfail(RR_E_ARG, "rank 0 needs a device frame buffer");
+    const int32_t block = o->block_rows > 0 ? o->block_rows : 8;
+    const int64_t W = cam->hsize / o->aa, H = cam->vsize / o->aa;
+    const int64_t max_rows = rows_of(H, 0, g->nranks, block);  // part 0 holds the most rows
+    const size_t count = (size_t)max_rows * (size_t)W * 3;       // doubles per (padded) tile
+    const int b = (int)(g->k & 1);
+    const int n = (int)g->subs.size();
+    if (g->root_here()) {
+        GHIP(hipSetDevice(g->devices[0]));
+        GHIP(g->recv[b].ensure(count * g->nranks * sizeof(double)));
+        if (stream) GHIP(hipEventRecord(g->ev_caller, (hipStream_t)stream));
+    }
+    for (int l = 0; l < n; ++l) {
+        GHIP(hipSetDevice(g->devices[l]));
+        const bool root = g->root_here() && l == 0;
+        if (!root) GHIP(g->tile[b][l].ensure(count * sizeof(double)));
+        void* t = root ? g->recv[b].p : g->tile[b][l].p;
+        // the gather that last read this buffer (two frames ago) must be done before it is overwritten
+        GHIP(hipStreamWaitEvent(g->render_st[l], g->ev_gathered[b][l], 0));
+        rr_render_opts so = *o;
+        so.part = g->rank0 + l;
+        so.nparts = g->nranks;
+        so.block_rows = block;
+        so.flags = RR_OUT_AVG | (o->flags & RR_NO_FRAME_TIMING);
+        int rc = rr_render_device(g->subs[l], cam, &so, nullptr, t, g->render_st[l]);
+        if (rc != RR_OK) return rc;
+        GHIP(hipEventRecord(g->ev_rendered[b][l], g->render_st[l]));
+        GHIP(hipStreamWaitEvent(g->comm_st[l], g->ev_rendered[b][l], 0));
+    }
+    // one gather per frame: rank 0 receives rank r's tile at offset r * count (its own in place)
+    GNCCL(ncclGroupStart());
+    for (int l = 0; l < n; ++l) {
+        const bool root = g->root_here() && l == 0;
+        void* send = root ? g->recv[b].p : g->tile[b][l].p;
+        GNCCL(ncclGather(send, root ? g->recv[b].p : nullptr, count, ncclFloat64, 0, g->comms[l], g->comm_st[l]));
+    }
+    GNCCL(ncclGroupEnd());
+    for (int l = 0; l < n; ++l) {
+        GHIP(hipSetDevice(g->devices[l]));
+        if (g->root_here() && l == 0) {
+            if (stream) GHIP(hipStreamWaitEvent(g->comm_st[0], g->ev_caller, 0));  // d_frame in the caller's order
+            GHIP(launch_unshuffle(static_cast<const double*>(g->recv[b].p), static_cast<double*>(d_frame), W, H,
+                                  g->nranks, block, max_rows, g->comm_st[0]));
+        }
+        GHIP(hipEventRecord(g->ev_gathered[b][l], g->comm_st[l]));
+    }
+    if (g->root_here() && stream) {
+        GHIP(hipSetDevice(g->devices[0]));
+        GHIP(hipStreamWaitEvent((hipStream_t)stream, g->ev_gathered[b][0], 0));
+    }
+    ++g->k;
+    return RR_OK;
+}
+
+int group_render(rr_group* g, const rr_camera* cam, const rr_render_opts* o, double* out_canvas, double* out_avg,
+                 rr_stats* stats) {
+    if (!cam || !o) return gfail(RR_E_ARG, "null camera/options");
+    if ((o->flags & RR_OUT_CANVAS) && out_canvas)
+        return gfail(RR_E_ARG, "multi-device contexts produce the f64 AA-averaged image only (RR_OUT_AVG)");
+    if (o->aa < 1 || cam->hsize <= 0 || cam->vsize <= 0 || cam->hsize % o->aa || cam->vsize % o->aa)
+        return gfail(RR_E_ARG, "camera size must be a positive multiple of aa");
+    const int64_t W = cam->hsize / o->aa, H = cam->vsize / o->aa;
+    if (g->root_here()) {
+        GHIP(hipSetDevice(g->devices[0]));
+        GHIP(g->frame.ensure((size_t)W * H * 3 * sizeof(double)));
+    }
+    rr_render_opts so = *o;
+    so.flags = RR_OUT_AVG;
+    int rc = group_render_gather(g, cam, &so, g->root_here() ? g->frame.p : nullptr, nullptr);
+    if (rc != RR_OK) return rc;
+    for (size_t l = 0; l < g->subs.size(); ++l) {
+        GHIP(hipSetDevice(g->devices[l]));
+        GHIP(hipStreamSynchronize(g->render_st[l]));
+        GHIP(hipStreamSynchronize(g->comm_st[l]));
+    }
+    if (g->root_here() && out_avg && (o->flags & RR_OUT_AVG)) {
+        GHIP(hipSetDevice(g->devices[0]));
+        GHIP(hipMemcpy(out_avg, g->frame.p, (size_t)W * H * 3 * sizeof(double), hipMemcpyDeviceToHost));
+    }
+    if (stats) return group_last_stats(g, stats);
+    return RR_OK;
+}
+
+int group_last_stats(rr_group* g, rr_stats* s) {
+    if (!s) return gfail(RR_E_ARG, "null stats");
+    std::memset(s, 0, sizeof(*s));
+    for (rr_ctx* c : g->subs) {  // sum over this process's devices
+        rr_stats t;
+        int rc = rr_last_stats(c, &t);
+        if (rc != RR_OK) return rc;
+        s->rays += t.rays;
+        s->shadow_rays += t.shadow_rays;
+        s->shade_events += t.shade_events;
+        s->n1n2_scans += t.n1n2_scans;
+        s->group_tests += t.group_tests;
+        s->group_hits += t.group_hits;
+        s->samples += t.samples;
+        s->prim_tests += t.prim_tests;
+        s->kernel_ms = std::max(s->kernel_ms, t.kernel_ms);
+        for (int k = 0; k < 3; ++k) {
+            s->exact_flops[k] += t.exact_flops[k];
+            s->wave_visits[k] += t.wave_visits[k];
+        }
+    }
+    return RR_OK;
+}
+
+rr_ctx* group_local(rr_group* g, int l) { return (l >= 0 && l < (int)g->subs.size()) ? g->subs[l] : nullptr; }
+
+int group_info(const rr_group* g, int32_t* nranks, int32_t* rank0, int32_t* nlocal) {
+    if (nranks) *nranks = g->nranks;
+    if (rank0) *rank0 = g->rank0;
+    if (nlocal) *nlocal = (int32_t)g->subs.size();
+    return RR_OK;
+}
+
+}  // namespace rr
+
+extern "C" int rr_rccl_unique_id(uint8_t* out, int32_t n) {
+    if (!out || n < (int32_t)sizeof(ncclUniqueId)) return gfail(RR_E_ARG, "rr_rccl_unique_id: need RR_RCCL_ID_BYTES bytes");
+    ncclUniqueId id;
+    GNCCL(ncclGetUniqueId(&id));
+    std::memcpy(out, &id, sizeof(id));
+    return RR_OK;
+}

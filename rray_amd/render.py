@@ -232,13 +232,51 @@ def device_count():
     return n.value
 
 
-class Renderer:
-    """One gfx950 device context (rr_ctx): scene in HBM + the wavefront kernels."""
+def rccl_unique_id():
+    """rr_rccl_unique_id: the bytes rank 0 shares with the other ranks before Renderer.rank(...)."""
+    buf = (C.c_uint8 * _lib.RCCL_ID_BYTES)()
+    check(lib().rr_rccl_unique_id(buf, _lib.RCCL_ID_BYTES))
+    return bytes(buf)
 
-    def __init__(self, device=0):
+
+class Renderer:
+    """A gfx950 render context (rr_ctx): scene in HBM + the wavefront kernels.  Renderer(d) drives one
+    device; Renderer.multi(ids) several devices of this process, Renderer.rank(d, n, r, uid) one rank of
+    a one-process-per-GPU group — both split each frame in row tiles and gather them with RCCL."""
+
+    def __init__(self, device=0, _handle=None):
         self.h = C.c_void_p()
-        check(lib().rr_create(device, C.byref(self.h)))
+        if _handle is not None:
+            self.h = _handle
+        else:
+            check(lib().rr_create(device, C.byref(self.h)))
         self.device = device
+
+    @classmethod
+    def multi(cls, device_ids):
+        ids = (C.c_int * len(device_ids))(*device_ids)
+        h = C.c_void_p()
+        check(lib().rr_create_multi(len(device_ids), ids, C.byref(h)))
+        return cls(device_ids[0], _handle=h)
+
+    @classmethod
+    def rank(cls, device, nranks, rank, unique_id):
+        uid = (C.c_uint8 * _lib.RCCL_ID_BYTES).from_buffer_copy(unique_id)
+        h = C.c_void_p()
+        check(lib().rr_create_rank(device, nranks, rank, uid, C.byref(h)))
+        return cls(device, _handle=h)
+
+    def info(self):
+        """(nranks, first global rank of this context, local devices)."""
+        a, b, c = C.c_int32(), C.c_int32(), C.c_int32()
+        check(lib().rr_context_info(self.h, C.byref(a), C.byref(b), C.byref(c)))
+        return a.value, b.value, c.value
+
+    def render_gather_device(self, cam, opts, d_frame, stream=None):
+        """Whole frame (row tiles over the group's devices + one RCCL gather) into d_frame on rank 0's
+        device, in `stream` order (asynchronous)."""
+        check(lib().rr_render_gather_device(self.h, C.byref(cam), C.byref(opts), C.c_void_p(d_frame) if d_frame else None,
+                                            C.c_void_p(stream) if stream else None))
 
     def close(self):
         if getattr(self, "h", None):
@@ -331,6 +369,12 @@ def render_scene_from_str(text, width, height, png_file, aa=1, device=0, obj_roo
     return res
 
 
-def render_scene_from_file(path, width, height, png_file, aa=1, device=0):
-    """scene_builder_yaml.rs:429-436 on the GPU (same error as the reference for a missing file)."""
+def render_scene_from_file(path, width, height, png_file, aa=1, device=0, devices=None):
+    """scene_builder_yaml.rs:429-436 on the GPU (same error as the reference for a missing file);
+    devices=[...] splits the frame over several GPUs (rr_create_multi)."""
+    if devices:
+        ids = (C.c_int * len(devices))(*devices)
+        check(lib().rr_render_scene_from_file_devices(path.encode(), width, height, png_file.encode(), aa, len(devices),
+                                                      ids))
+        return
     check(lib().rr_render_scene_from_file(path.encode(), width, height, png_file.encode(), aa, device))

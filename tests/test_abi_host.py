@@ -228,3 +228,37 @@ def test_png_texture_decoder_matches_pil(R):
     with pytest.raises(R.RRError) as e:  # JPEG (examples/Texturelabs_Stone_138M.jpg): host-side decode only
         R.YamlScene(text.replace("png/tex_grid.png", "teapot-low.obj"), 8, 8, 1, obj_root=GOLDEN)
     assert e.value.code == R._lib.RR_E_LIMIT
+
+
+def test_group_contexts_need_a_device(R):
+    """rr_create_multi / rr_create_rank validate their arguments and, like rr_create, have no CPU
+    fallback (the multi-GPU path itself runs in tests/test_gpu_multi.py)."""
+    with pytest.raises(R.RRError) as e:
+        R.Renderer.multi([])
+    assert e.value.code == -1  # RR_E_ARG
+    with pytest.raises(R.RRError) as e:
+        R.Renderer.rank(0, 2, 5, bytes(R._lib.RCCL_ID_BYTES))
+    assert e.value.code == -1
+    if R.device_count() == 0:
+        with pytest.raises(R.RRError) as e:
+            R.Renderer.multi([0])
+        assert e.value.code == -2  # RR_E_HIP
+
+
+def test_cli_argument_errors():
+    """The drop-in CLI's clap-style errors (main.rs:13-45) and the missing-file panic
+    (scene_builder_yaml.rs:434) as an exit code — none of these touch the GPU."""
+    import subprocess
+
+    cli = os.path.join(ROOT, "rray_amd", "bin", "rray")
+    r = subprocess.run([cli, "-W", "10"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "--scene <SCENE>" in r.stderr
+    r = subprocess.run([cli, "-s", "x.yaml", "-a", "6"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "less than or equal to 5" in r.stderr
+    r = subprocess.run([cli, "-s", "x.yaml", "-W", "-3"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2
+    r = subprocess.run([cli, "-s", os.path.join(ROOT, "no_such_scene.yaml")], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 1 and "File does not exist" in r.stderr
+    r = subprocess.run([cli, "-V"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.startswith("rray")

@@ -1,0 +1,154 @@
+"""GPU tests of the multi-device contexts (rr_create_multi / rr_create_rank: row tiles + one RCCL
+gather) and of the drop-in CLI end to end (main.rs:49-77 -> PNG on disk).
+
+The GPU box has one MI355X, so the groups here have one device / one rank: they exercise the whole
+path through the C ABI (tile render into the gather buffer, ncclGather on a 1-rank communicator, the
+un-interleave kernel, double-buffered pipelining); the partition arithmetic for N > 1 is covered by
+test_multi_part_tiles_are_bit_identical (GPU) and tests/test_dist_gloo.py (CPU).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCENES = os.path.join(ROOT, "scenes")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+CLI = os.path.join(ROOT, "rray_amd", "bin", "rray")
+
+
+@pytest.fixture(scope="module")
+def R():
+    import rray_amd
+
+    if rray_amd.device_count() < 1:
+        pytest.fail("no HIP device visible (GPU tests must run on the MI355X box)")
+    return rray_amd
+
+
+@pytest.fixture(scope="module")
+def single(R):
+    r = R.Renderer(0)
+    yield r
+    r.close()
+
+
+def _scene(R, name, W, H, aa):
+    text = open(os.path.join(SCENES, name)).read()
+    return R.YamlScene(text, W, H, aa, obj_root=SCENES)
+
+
+@pytest.mark.parametrize("kind", ["multi", "rank"])
+def test_group_context_matches_single_device(R, single, kind):
+    """A 1-device group (ncclCommInitAll) and a 1-rank group (ncclCommInitRank from
+    rr_rccl_unique_id) render the same image as the plain context, bit for bit."""
+    scene = _scene(R, "c3_s1024_reflect.yaml", 48, 40, 2)
+    single.upload(scene)
+    ref = single.render(scene.camera, aa=2)
+    g = R.Renderer.multi([0]) if kind == "multi" else R.Renderer.rank(0, 1, 0, R.rccl_unique_id())
+    try:
+        assert g.info() == (1, 0, 1)
+        g.upload(scene)
+        got = g.render(scene.camera, aa=2)
+        assert np.array_equal(got["avg"], ref["avg"])
+        for k in ("rays", "shadow_rays", "shade_events"):
+            assert got["stats"][k] == ref["stats"][k], k
+    finally:
+        g.close()
+
+
+def test_group_rejects_part_and_canvas(R):
+    scene = _scene(R, "c2_s1024.yaml", 32, 16, 1)
+    g = R.Renderer.multi([0])
+    try:
+        g.upload(scene)
+        with pytest.raises(R.RRError) as e:
+            g.render(scene.camera, aa=1, canvas=True)
+        assert e.value.code == -1
+        with pytest.raises(R.RRError) as e:
+            g.render(scene.camera, aa=1, part=0, nparts=2)
+        assert e.value.code == -1
+        with pytest.raises(R.RRError) as e:  # a group has no single-device entry point
+            g.render_device(scene.camera, R._lib.RenderOpts(1, 5, 0, 0, 0, 1, 8, R._lib.RR_OUT_AVG), None, 1, None)
+        assert e.value.code == -1
+    finally:
+        g.close()
+    with pytest.raises(R.RRError):
+        R.Renderer.multi([0, 0])  # distinct devices only
+
+
+def test_pipelined_gathers_keep_frames_apart(R, single):
+    """rr_render_gather_device is asynchronous and double-buffers its tiles: three frames from two
+    cameras enqueued back to back land in their own buffers unchanged."""
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    W, H, aa = 64, 48, 2
+    scene = _scene(R, "c3_s1024_reflect.yaml", W, H, aa)
+    cam_a = scene.camera
+    cam_b = R.camera(cam_a.hsize, cam_a.vsize, cam_a.field_of_view * 0.75, list(cam_a.transform))
+    single.upload(scene)
+    ref_a = single.render(cam_a, aa=aa)["avg"]
+    ref_b = single.render(cam_b, aa=aa)["avg"]
+    assert not np.array_equal(ref_a, ref_b)
+    g = R.Renderer.rank(0, 1, 0, R.rccl_unique_id())
+    bufs = []
+    try:
+        g.upload(scene)
+        nbytes = ref_a.size * 8
+        for _ in range(3):
+            d = ctypes.c_void_p()
+            assert hip.hipMalloc(ctypes.byref(d), ctypes.c_size_t(nbytes)) == 0
+            bufs.append(d)
+        opts = R._lib.RenderOpts(aa, 5, 0, 0, 0, 1, 8, R._lib.RR_OUT_AVG | R._lib.RR_NO_FRAME_TIMING)
+        for cam, d in zip((cam_a, cam_b, cam_a), bufs):
+            g.render_gather_device(cam, opts, d.value, None)
+        assert hip.hipDeviceSynchronize() == 0
+        outs = []
+        for d in bufs:
+            out = np.empty_like(ref_a)
+            assert hip.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), d, ctypes.c_size_t(nbytes), 2) == 0
+            outs.append(out)
+    finally:
+        for d in bufs:
+            hip.hipFree(d)
+        g.close()
+    assert np.array_equal(outs[0], ref_a)
+    assert np.array_equal(outs[1], ref_b)
+    assert np.array_equal(outs[2], ref_a)
+
+
+def _png(path):
+    PIL = pytest.importorskip("PIL.Image")
+    return np.asarray(PIL.open(path).convert("RGB"))
+
+
+@pytest.mark.parametrize("yaml,png,aa,cwd", [
+    ("objects_cube.yaml", "png/objects_cube.png", 3, GOLDEN),
+    ("example1.yaml", "example1/example1.png", 3, os.path.join(GOLDEN, "example1")),
+])
+def test_cli_renders_reference_png(tmp_path, yaml, png, aa, cwd):
+    """`rray -W 800 -H 400 -s <scene> -o out.png -a 3` (main.rs:49-77 -> render_scene_from_file,
+    scene_builder_yaml.rs:429-436): the PNG written to disk equals the reference renderer's own."""
+    out = tmp_path / "out.png"
+    r = subprocess.run([CLI, "-W", "800", "-H", "400", "-s", yaml, "-o", str(out), "-a", str(aa)], cwd=cwd,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got, ref = _png(out), _png(os.path.join(GOLDEN, png))
+    diff = int((got != ref).any(axis=2).sum())
+    print(f"CLI {yaml}: {diff} of {ref.shape[0] * ref.shape[1]} pixels differ")
+    assert diff == 0
+
+
+def test_cli_multi_device_env(tmp_path):
+    """RRAY_DEVICES selects a multi-device context in the CLI (here: the one device of the box)."""
+    out1, out2 = tmp_path / "a.png", tmp_path / "b.png"
+    args = ["-W", "200", "-H", "100", "-s", "objects_cone.yaml", "-a", "2"]
+    r1 = subprocess.run([CLI] + args + ["-o", str(out1)], cwd=GOLDEN, capture_output=True, text=True, timeout=120)
+    env = dict(os.environ, RRAY_DEVICES="0")
+    r2 = subprocess.run([CLI] + args + ["-o", str(out2)], cwd=GOLDEN, capture_output=True, text=True, timeout=120,
+                        env=env)
+    assert r1.returncode == 0 and r2.returncode == 0, (r1.stderr, r2.stderr)
+    assert np.array_equal(_png(out1), _png(out2))
