@@ -293,10 +293,18 @@ uint64_t splitmix64(uint64_t x) {
 
 }  // namespace
 
+// Deterministic stand-in for thread_rng (light.rs:57-59), shared bit for bit with the HIP kernels
+// (device_core.inc jitter_base / jitter_value): a 64-bit mix of (seed, global sample id, recursion
+// path) per shading event, then a 32-bit lowbias32 mix per value of (light, cell sample, u/v).
 extern "C" double orc_jitter(uint64_t seed, uint64_t sample, uint32_t path, uint32_t light, uint32_t s, uint32_t which) {
-    uint64_t k = ((uint64_t)path << 40) ^ ((uint64_t)light << 32) ^ ((uint64_t)s << 1) ^ (uint64_t)which;
-    uint64_t h = splitmix64(seed ^ splitmix64(sample ^ splitmix64(k)));
-    return (double)(h >> 11) * (1.0 / 9007199254740992.0);
+    const uint32_t base = (uint32_t)(splitmix64(seed ^ splitmix64(sample ^ ((uint64_t)path << 40))) >> 32);
+    uint32_t x = base ^ ((light << 21) | (s << 1) | which);
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return (double)x * (1.0 / 4294967296.0);
 }
 
 struct Texture {  // texture.rs:6-11 (RgbaImage after to_rgba8)

@@ -23,7 +23,8 @@ ARCH = "gfx950"
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
           "-I" + os.path.join(ROOT, "include")]
 DEVICE = ["--offload-arch=" + ARCH, "-mllvm", "-disable-promote-alloca-to-lds"]
-SOURCES = ["render.hip", "api.cpp", "multi.cpp", "flatten.cpp", "frontend.cpp", "yaml.cpp", "png.cpp"]
+LEVEL_UNITS = [f"render_levels_g{g}_{lc}.hip" for g in (2, 1, 0) for lc in ("lds", "gl")]  # slowest first
+SOURCES = LEVEL_UNITS + ["render.hip", "api.cpp", "multi.cpp", "flatten.cpp", "frontend.cpp", "yaml.cpp", "png.cpp"]
 
 
 def _deps_mtime():
@@ -55,8 +56,8 @@ def build_variant(name, defines, verbose=False):
     out_dir = os.path.join(HERE, "_exp", name)
     os.makedirs(out_dir, exist_ok=True)
     flags = ["-D" + d for d in defines]
-    objs = []
-    for src in SOURCES:
+
+    def one(src):
         o = os.path.join(out_dir, os.path.splitext(src)[0] + ".o")
         pre = [HIPCC, "-x", "hip"] if src.endswith(".cpp") else [HIPCC]
         cmd = pre + COMMON + DEVICE + flags + ["-c", os.path.join(CSRC, src), "-o", o]
@@ -65,7 +66,10 @@ def build_variant(name, defines, verbose=False):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"compile failed: {src}\n{r.stderr}")
-        objs.append(o)
+        return o
+
+    with cf.ThreadPoolExecutor(min(len(SOURCES), max(1, min(16, os.cpu_count() or 1)))) as ex:
+        objs = list(ex.map(one, SOURCES))
     lib = os.path.join(out_dir, "librray_amd.so")
     r = subprocess.run([HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", lib] + objs + ["-lz"], capture_output=True,
                        text=True)
@@ -79,7 +83,7 @@ def build(verbose=False, jobs=None):
     os.makedirs(LIBDIR, exist_ok=True)
     os.makedirs(BINDIR, exist_ok=True)
     dm = _deps_mtime()
-    jobs = jobs or min(len(SOURCES), max(1, min(8, os.cpu_count() or 1)))
+    jobs = jobs or min(len(SOURCES), max(1, min(16, os.cpu_count() or 1)))
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, dm, verbose), SOURCES))
     newest = max(os.path.getmtime(o) for o in objs)

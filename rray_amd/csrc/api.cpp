@@ -510,6 +510,8 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     S.n_nodes = (int32_t)c->host.nodes.size();
     S.n_lights = (int32_t)c->host.lights.size();
     S.has_transparent = c->host.has_transparent;
+    S.has_area = 0;
+    for (const rr::DevLight& l : c->host.lights) S.has_area |= l.kind == RR_LIGHT_AREA ? 1 : 0;
     S.complex_patterns = c->host.complex_patterns;
     S.has_groups = c->host.groups.empty() ? 0 : 1;
     S.general = (c->host.has_csg || c->host.has_quad) ? 1 : 0;

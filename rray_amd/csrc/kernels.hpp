@@ -103,6 +103,10 @@ struct KernelProf {
 };
 
 hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t stream, KernelProf* prof = nullptr);
+// one (G, LC) variant of a level's kernels (render_levels.inc), instantiated in its own translation
+// unit render_levels_g<G>_<lds|gl>.hip; G = 0 flat, 1 groups, 2 general; LC = culls staged in LDS
+template <int G, bool LC>
+void launch_level_t(const DevScene& S, const LevelArgs& A, hipStream_t stream, KernelProf* prof);
 hipError_t launch_combine(const CombArgs& C, hipStream_t stream, KernelProf* prof = nullptr);
 hipError_t launch_aa(const double* canvas, double* out, int64_t width, int64_t rows, int32_t aa, hipStream_t stream,
                      KernelProf* prof = nullptr);

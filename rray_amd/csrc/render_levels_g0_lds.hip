@@ -1,0 +1,16 @@
+// render_levels_g0_lds.hip — level kernels for G = 0 (flat scenes), culls staged in LDS.
+// One (G, LC) variant per translation unit so the kernel variants compile in parallel (render_levels.inc).
+#include <cstdlib>
+
+#include "device_core.inc"
+#include "kernels.hpp"
+#include "wavefront.hpp"
+
+namespace rr {
+
+#include "render_common.inc"
+#include "render_levels.inc"
+
+template void launch_level_t<0, true>(const DevScene&, const LevelArgs&, hipStream_t, KernelProf*);
+
+}  // namespace rr

@@ -134,7 +134,7 @@ struct DevScene {
     const uint32_t* texels;
     int32_t n_nodes, n_lights;
     int32_t n_chunks;
-    int32_t pad2;
+    int32_t has_area;         // some light is an area light (the shade kernels stage its samples in LDS)
     int32_t has_transparent;  // any material with transparency != 0 (enables the n1/n2 walk)
     int32_t has_groups;
     int32_t general;          // CSGs or cylinders / cones present: the kernels' G = 2 variant
