@@ -253,6 +253,8 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             A.parent_comb = d > 0 ? c->comb[d - 1].as<rr::CombRec>() : nullptr;
             A.comb_ext = ext && children_possible ? c->comb_ext[d].as<rr::CombExt>() : nullptr;
             A.parent_ext = ext && d > 0 ? c->comb_ext[d - 1].as<rr::CombExt>() : nullptr;
+            for (int q = 0; q <= RR_MAX_DEPTH; ++q)
+                A.chain[q] = q + 1 < p.levels ? c->comb[q].as<rr::ChainRec>() : nullptr;
             A.out = out;
             A.avg = avg;
             A.avg_f32 = avg_f32;
@@ -289,8 +291,9 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             }
 #endif
         }
-        // bottom-up shade_hit sums of the events with children (scene.rs:172-177)
-        for (int d = p.levels - 2; d >= 0; --d) {
+        // bottom-up shade_hit sums of the events with children (scene.rs:172-177); fused levels finish
+        // their chains in the kernels
+        for (int d = p.levels - 2; d >= 0 && !rr::fused_levels(c->S); --d) {
             rr::CombArgs C{};
             C.level = d;
             C.n = p.cap[d];

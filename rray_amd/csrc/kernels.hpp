@@ -32,6 +32,7 @@ struct LevelArgs {
     CombRec* parent_comb;    // level - 1 (children deliver into their parent's slot)
     CombExt* comb_ext;       // refraction halves (null when no material is transparent)
     CombExt* parent_ext;
+    ChainRec* chain[RR_MAX_DEPTH + 1];  // FUSED levels: each level's pending surface sums (in the comb buffers)
     double* out;             // level 0: canvas / color_at results (3 doubles per local sample), or null
     void* avg;               // aa == 1: the averaged image written directly (canvas.rs:85-96 with aa = 1)
     int32_t avg_f32;         // avg holds floats (RR_OUT_AVG_F32)
@@ -103,6 +104,9 @@ struct KernelProf {
 };
 
 hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t stream, KernelProf* prof = nullptr);
+// trace + shade run as one kernel per level (no transparent material, so no n1/n2 walk between them);
+// those levels finish their reflection chains themselves and need no combine pass
+bool fused_levels(const DevScene& S);
 // one (G, LC) variant of a level's kernels (render_levels.inc), instantiated in its own translation
 // unit render_levels_g<G>_<lds|gl>.hip; G = 0 flat, 1 groups, 2 general; LC = culls staged in LDS
 template <int G, bool LC>

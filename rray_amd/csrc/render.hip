@@ -97,6 +97,8 @@ hipEvent_t KernelProf::get() {
 }
 
 
+bool fused_levels(const DevScene& S) { return !S.has_transparent && !std::getenv("RRAY_UNFUSED"); }
+
 hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t st, KernelProf* prof) {
     if (A.n <= 0) return hipSuccess;
     const int g = S.general ? 2 : S.has_groups ? 1 : 0;  // G: flat / groups / general (CSG, 4-entry leaves)

@@ -42,6 +42,15 @@ struct CombExt {
     double transp, R;
 };
 static_assert(sizeof(CombRec) == 64, "CombRec layout");
+// Scenes without transparency (the FUSED kernels): an event has at most one child, its reflection,
+// so no combine pass runs — the chain's leaf folds every ancestor's record on its way up.
+struct alignas(16) ChainRec {
+    double surf[3];
+    double refl;      // the material's reflective
+    int32_t parent;   // event index at level - 1 (-1 at level 0)
+    int32_t pad[3];
+};
+static_assert(sizeof(ChainRec) == 48 && sizeof(ChainRec) <= sizeof(CombRec), "ChainRec layout");
 enum { CF_HIT = 1, CF_REFRACT_CHILD = 2 };
 
 // per-level device counters

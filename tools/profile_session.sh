@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOTDIR=$(pwd)
-OUT=$ROOTDIR/gpurun_out/prof
+OUT=$ROOTDIR/gpurun_out/${PROF_DIR:-prof}
 WL=${WL:-c2_s1024}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -21,9 +21,14 @@ run() {  # name, timeout, rocprof args...  (PSTEPS: steps of this pass)
   echo "== $name rc=$rc"; tail -n 3 "$OUT/$name.log"
   return $rc
 }
-PSTEPS=$STEPS PWARM=5 run kt 300 --kernel-trace --stats || exit 1
-run pmc_fetch 300 --pmc FETCH_SIZE || exit 1
-run pmc_write 300 --pmc WRITE_SIZE || exit 1
-run pmc_sq 300 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU || exit 1
-run pmc_sq2 300 --pmc SQ_WAVES SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH GRBM_GUI_ACTIVE
+PASSES=${PASSES:-kt fetch write sq sq2}  # subset to run (each pass is its own rocprofv3 run)
+for p in $PASSES; do
+  case $p in
+    kt) PSTEPS=$STEPS PWARM=5 run kt 300 --kernel-trace --stats || exit 1;;
+    fetch) run pmc_fetch 300 --pmc FETCH_SIZE || exit 1;;
+    write) run pmc_write 300 --pmc WRITE_SIZE || exit 1;;
+    sq) run pmc_sq 300 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU || exit 1;;
+    sq2) run pmc_sq2 300 --pmc SQ_WAVES SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH GRBM_GUI_ACTIVE || exit 1;;
+  esac
+done
 find "$OUT" -name "*.csv" | head -50
