@@ -53,6 +53,7 @@ enum { RR_LIGHT_POINT = 0, RR_LIGHT_AREA = 1 };
 
 #define RR_MAX_DEPTH 8          /* max `remaining` (render uses 5, camera.rs:113) */
 #define RR_MAX_GROUP_DEPTH 6    /* nested group levels */
+#define RR_MAX_AREA_LEVEL 1024  /* area light `level` (level^2 jittered samples per shading event) */
 #define RR_MAX_PATTERN_DEPTH 8  /* nested pattern levels */
 #define RR_MAX_CSG_ENTRIES 32   /* intersections one CSG subtree can produce for one ray */
 #define RR_MAX_OCTAVES 64       /* octave_perlin octaves (noise.rs:11-29) */

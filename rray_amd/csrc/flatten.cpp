@@ -382,6 +382,10 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
             err = "area light with level <= 0";
             return RR_E_SCENE;
         }
+        if (l.kind == RR_LIGHT_AREA && l.level > RR_MAX_AREA_LEVEL) {  // level^2 cell samples per shading event
+            err = "area light level exceeds RR_MAX_AREA_LEVEL";
+            return RR_E_LIMIT;
+        }
         out.lights.push_back(l);
     }
 

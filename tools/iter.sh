@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  timeout -k 10 400 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread \
+  timeout -k 10 400 python -u -m pytest tests -m gpu -x -q -s -p no:cacheprovider --timeout 120 --timeout-method thread \
     ${TESTK:+-k "$TESTK"} > gpurun_out/t.log 2>&1; rc=$?
   echo "tests rc=$rc"; tail -3 gpurun_out/t.log
   [ $rc -ne 0 ] && exit $rc
