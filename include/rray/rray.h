@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 5
+#define RR_ABI_VERSION 6
 
 /* error codes */
 #define RR_OK 0
@@ -36,7 +36,10 @@ extern "C" {
 #define RR_E_NONAFFINE (-4)  /* inverse transform with row 3 != (0,0,0,1) */
 #define RR_E_LIMIT (-5)      /* exceeds a compiled limit (depth, pattern nesting) */
 #define RR_E_IO (-6)         /* file missing / unreadable / unwritable */
-#define RR_E_NAN (-7)        /* NaN intersection t: reference panics in sort (scene.rs:104) */
+#define RR_E_NAN (-7)        /* NaN intersection t in a list of >= 2 entries: the reference panics in
+                                Vec::sort_by(partial_cmp().unwrap()) (scene.rs:104, group.rs:88, csg.rs:231).
+                                rr_render / rr_color_at return it after writing their outputs; for
+                                rr_render_device see rr_stats.nan_rays. */
 
 /* object kinds — Sphere, Plane, Group, Triangle, SmoothTriangle, Cube, Cylinder, Cone, Csg, Torus
  * (src/raytracer/object/) */
@@ -146,6 +149,9 @@ typedef struct {
     double kernel_ms;       /* render + AA kernels, HIP events (0 with RR_NO_FRAME_TIMING) */
     uint64_t exact_flops[3];  /* f64 flops of those tests (SURVEY §8d model) per walk: trace, shadow, n1n2 */
     uint64_t wave_visits[3];  /* wave-level node visits (exact test issued for a 64-lane wave), same order */
+    /* ABI 6: rays whose intersection list (as far as the walk computed it) held a NaN t among >= 2
+       entries — where the reference panics; > 0 makes rr_render return RR_E_NAN */
+    uint64_t nan_rays;
 } rr_stats;
 
 typedef struct rr_ctx rr_ctx;

@@ -710,12 +710,15 @@ AABB get_aabb(orc_world* w, int id) {
 }
 
 void sort_xs(std::vector<Intersection>& xs, Ctx& ctx) {
-    // Vec::sort_by(partial_cmp().unwrap()) is a stable sort that panics on NaN
-    for (auto& x : xs)
-        if (std::isnan(x.t)) {
-            ctx.nan = true;
-            ctx.st.nan_sorts++;
-        }
+    // Vec::sort_by(partial_cmp().unwrap()) is a stable sort that panics on a NaN comparison; a list of
+    // fewer than two entries is never compared
+    if (xs.size() >= 2)
+        for (auto& x : xs)
+            if (std::isnan(x.t)) {
+                ctx.nan = true;
+                ctx.st.nan_sorts++;
+                break;
+            }
     std::stable_sort(xs.begin(), xs.end(), [](const Intersection& a, const Intersection& b) { return a.t < b.t; });
 }
 

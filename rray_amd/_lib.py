@@ -54,7 +54,7 @@ class Stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("shade_events", C.c_uint64),
                 ("n1n2_scans", C.c_uint64), ("group_tests", C.c_uint64), ("group_hits", C.c_uint64),
                 ("samples", C.c_uint64), ("prim_tests", C.c_uint64), ("kernel_ms", C.c_double),
-                ("exact_flops", C.c_uint64 * 3), ("wave_visits", C.c_uint64 * 3)]
+                ("exact_flops", C.c_uint64 * 3), ("wave_visits", C.c_uint64 * 3), ("nan_rays", C.c_uint64)]
 
     def as_dict(self):
         out = {}

@@ -332,6 +332,12 @@ void collect_stats(rr_ctx* c, rr_stats* s) {
         s->exact_flops[k] = h[rr::C_FLOPS_TRACE + k];
         s->wave_visits[k] = h[rr::C_VISITS_TRACE + k];
     }
+    s->nan_rays = h[rr::C_NAN];
+}
+int nan_fail(uint64_t n) {
+    return fail(RR_E_NAN, std::to_string(n) +
+                              " ray(s) met a NaN intersection t in a list of >= 2 entries: the reference panics in "
+                              "Vec::sort_by(partial_cmp().unwrap()) (scene.rs:104)");
 }
 
 int resolve_prof(rr_ctx* c) {
@@ -720,8 +726,11 @@ int rr_render(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, double* 
     if (want_avg)
         HIPCHK(hipMemcpyAsync(out_avg, c->qout.p, W * rows * 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (stats) return rr_last_stats(c, stats);
-    return RR_OK;
+    rr_stats local;
+    rc = rr_last_stats(c, stats ? stats : &local);
+    if (rc != RR_OK) return rc;
+    const uint64_t nan = (stats ? stats : &local)->nan_rays;
+    return nan ? nan_fail(nan) : RR_OK;
 }
 
 int rr_color_at(rr_ctx* c, int64_t n, const double* origins, const double* directions, int32_t remaining,
@@ -758,8 +767,10 @@ int rr_color_at(rr_ctx* c, int64_t n, const double* origins, const double* direc
     c->epoch = saved_epoch;
     if (rc != RR_OK) return rc;
     HIPCHK(hipMemcpyAsync(out_rgb, c->qout.p, n * 3 * sizeof(double), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    return RR_OK;
+    HIPCHK(hipMemcpy(c->h_counters, frame_counters(c, 2), kCounterBytes, hipMemcpyDeviceToHost));
+    rr_stats q;
+    collect_stats(c, &q);
+    return q.nan_rays ? nan_fail(q.nan_rays) : RR_OK;
 }
 
 int rr_is_shadowed(rr_ctx* c, int64_t n, const double* points, const double* light_positions, int32_t* out) {

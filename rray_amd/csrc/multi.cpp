@@ -325,7 +325,13 @@ int group_render(rr_group* g, const rr_camera* cam, const rr_render_opts* o, dou
         GHIP(hipSetDevice(g->devices[0]));
         GHIP(hipMemcpy(out_avg, g->frame.p, (size_t)W * H * 3 * sizeof(double), hipMemcpyDeviceToHost));
     }
-    if (stats) return group_last_stats(g, stats);
+    rr_stats local;
+    rc = group_last_stats(g, stats ? stats : &local);
+    if (rc != RR_OK) return rc;
+    const uint64_t nan = (stats ? stats : &local)->nan_rays;
+    if (nan)
+        return gfail(RR_E_NAN, std::to_string(nan) + " ray(s) met a NaN intersection t in a list of >= 2 entries "
+                                                     "(the reference panics in sort_by, scene.rs:104)");
     return RR_OK;
 }
 
@@ -345,6 +351,7 @@ int group_last_stats(rr_group* g, rr_stats* s) {
         s->samples += t.samples;
         s->prim_tests += t.prim_tests;
         s->kernel_ms = std::max(s->kernel_ms, t.kernel_ms);
+        s->nan_rays += t.nan_rays;
         for (int k = 0; k < 3; ++k) {
             s->exact_flops[k] += t.exact_flops[k];
             s->wave_visits[k] += t.wave_visits[k];

@@ -75,7 +75,7 @@ __global__ void __launch_bounds__(256) shadow_query_kernel(DevScene S, const dou
     if (LC) stage_culls(S);
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = i < n;
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     V3 p = mk(0, 0, 0), l = mk(0, 0, 1);
     if (valid) {
         p = mk(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]);

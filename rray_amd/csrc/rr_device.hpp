@@ -166,6 +166,7 @@ enum Counter {
     C_VISITS_TRACE,  // node visits x 64 (one per lane of a wave that ran a candidate's exact test)
     C_VISITS_SHADOW,
     C_VISITS_N1N2,
+    C_NAN,  // rays whose intersection list holds a NaN t among >= 2 entries (the reference's sort panics)
     C_COUNT
 };
 // Counters live in RR_CNT_SLOTS copies (slot = blockIdx % RR_CNT_SLOTS, RR_CNT_STRIDE u64 each) so

@@ -302,3 +302,72 @@ def test_device_render_without_frame_timing(renderer, R):
         assert np.array_equal(out, ref), flags
         assert (st["kernel_ms"] > 0) == timed, st["kernel_ms"]
         assert st["rays"] == 64 * 40
+
+
+NAN_CAMERA = "camera: {fov: 60, from: [0, 1, -5], to: [0, 1, -5], up: [0, 1, 0]}\n"  # from == to: NaN view
+
+
+def _nan_scene(objects):
+    return (NAN_CAMERA + "lights:\n  - type: point\n    color: [1, 1, 1]\n    position: [-10, 10, -10]\nscene:\n" +
+            objects)
+
+
+def test_nan_intersection_returns_rr_e_nan(renderer, R):
+    """from == to makes view_transform's forward 0/0 (camera.rs view_transform), so every camera ray
+    is NaN.  Two planes then give each ray a list of two NaN entries, which Vec::sort_by(partial_cmp()
+    .unwrap()) panics on (scene.rs:104): rr_render returns RR_E_NAN (the oracle flags the same
+    render), and so does one sphere (a NaN discriminant is not < 0: two NaN entries, sphere.rs:64-78).
+    One plane gives one-entry lists the sort never compares: it renders without an error, as in the
+    reference."""
+    from oracle.scene_yaml import build_from_yaml
+
+    for objs in ("  - type: plane\n  - type: plane\n    transforms: [{type: translate, amount: [0, -1, 0]}]\n",
+                 "  - type: sphere\n"):
+        text = _nan_scene(objs)
+        scene = R.YamlScene(text, 16, 8, 1)
+        renderer.upload(scene)
+        with pytest.raises(R.RRError) as ei:
+            renderer.render(scene.camera, aa=1)
+        assert ei.value.code == -7, str(ei.value)  # RR_E_NAN
+        st = renderer.last_stats()
+        assert st["nan_rays"] == 16 * 8, st
+        o, cam = build_from_yaml(text, 16, 8, 1)
+        with pytest.raises(RuntimeError, match="panic"):
+            o.render(cam, max_depth=5)
+    for objs in ("  - type: plane\n",):
+        text = _nan_scene(objs)
+        scene = R.YamlScene(text, 16, 8, 1)
+        renderer.upload(scene)
+        got = renderer.render(scene.camera, aa=1)
+        assert got["stats"]["nan_rays"] == 0
+        o, cam = build_from_yaml(text, 16, 8, 1)
+        canvas, _ = o.render(cam, max_depth=5)
+        assert np.array_equal(got["avg"], o.aa_average(canvas, 1), equal_nan=True)
+
+
+def test_area_light_png_statistically(renderer, R):
+    """examples/area_light.png is one draw of the reference's thread_rng jitter (light.rs:47-65), rendered
+    800x400 at aa=4 (the aa that reproduces it; aa 1-3 and 5-6 leave >30 000 jitter-free pixels
+    different).  Eight jitter seeds of the GPU render: pixels whose quantised colour is the same under
+    every seed do not depend on the jitter (fully lit, umbra, sky) and must equal the reference's —
+    allowed: 0.1 % of them off by <= 2 levels (pixels whose rare jitter dependence eight seeds did not
+    expose).  Penumbra pixels: the reference's value must lie inside the seeds' range +-2 levels for
+    >= 99.5 % of them, and the mean |reference - seed mean| must stay below one level."""
+    PIL = pytest.importorskip("PIL.Image")
+    text = open(os.path.join(SCENES, "c5_area_light.yaml")).read()  # byte-identical to examples/area_light.yaml
+    aa = 4
+    scene = R.YamlScene(text, 800, 400, aa, obj_root=GOLDEN)
+    renderer.upload(scene)
+    Q = np.stack([R.quantize(renderer.render(scene.camera, aa=aa, seed=s)["avg"])[..., :3].astype(np.int32)
+                  for s in range(8)])
+    ref = np.asarray(PIL.open(os.path.join(GOLDEN, "png", "area_light.png")).convert("RGB")).astype(np.int32)
+    stable = (Q == Q[0]).all(axis=0).all(axis=2)
+    d = np.abs(Q[0] - ref).max(axis=2)[stable]
+    pen = ~stable
+    inside = ((ref >= Q.min(axis=0) - 2) & (ref <= Q.max(axis=0) + 2)).all(axis=2)[pen]
+    mean_dev = float(np.abs(ref - Q.mean(axis=0))[pen].mean())
+    print(f"area_light.png aa=4: {int(stable.sum())} jitter-free px, {int((d > 0).sum())} differ (max {int(d.max())}); "
+          f"{int(pen.sum())} penumbra px, {float(inside.mean()):.4f} inside the seed range, mean dev {mean_dev:.3f}")
+    assert stable.sum() > 300000
+    assert (d > 0).sum() <= 0.001 * d.size and d.max() <= 2
+    assert inside.mean() >= 0.995 and mean_dev < 1.0

@@ -533,3 +533,22 @@ def test_torus_intersections(oracle_mod):
     assert o.local_intersect(t, (0.0, 0.0, -5.0, 1.0), (0.0, 0.0, 1.0, 0.0)) == []
     xs = o.local_intersect(t, (-5.0, 0.0, 0.0, 1.0), (1.0, 0.0, 0.0, 0.0))
     assert [round(x[0], 9) for x in xs] == [3.75, 4.25, 5.75, 6.25]
+
+
+def test_oracle_nan_sort_rule():
+    """Vec::sort_by(partial_cmp().unwrap()) panics only when it compares a NaN: a list of >= 2 entries
+    holding a NaN t (scene.rs:104).  A NaN camera (from == to) against two planes panics; against one
+    plane (one-entry lists, never compared) it renders; one sphere gives two NaN entries and panics."""
+    import pytest
+
+    from oracle.scene_yaml import build_from_yaml
+
+    head = ("camera: {fov: 60, from: [0, 1, -5], to: [0, 1, -5], up: [0, 1, 0]}\nlights:\n  - type: point\n"
+            "    color: [1, 1, 1]\n    position: [-10, 10, -10]\nscene:\n")
+    for objs in ("  - type: plane\n  - type: plane\n", "  - type: sphere\n"):
+        o, cam = build_from_yaml(head + objs, 8, 4, 1)
+        with pytest.raises(RuntimeError, match="panic"):
+            o.render(cam, max_depth=5)
+    o, cam = build_from_yaml(head + "  - type: plane\n", 8, 4, 1)
+    canvas, st = o.render(cam, max_depth=5)
+    assert st["nan_sorts"] == 0
