@@ -51,9 +51,9 @@ def _compile(src, deps_mtime, verbose):
 
 
 def build_variant(name, defines, verbose=False):
-    """Experiment build (e.g. RR_STAMPS phase timers) into rray_amd/_exp/<name>/librray_amd.so; select it
+    """Experiment build (e.g. RR_STAMPS phase timers) into abtest/<name>/librray_amd.so; select it
     at run time with RRAY_LIB=<path>.  Never used by the product path."""
-    out_dir = os.path.join(HERE, "_exp", name)
+    out_dir = os.path.join(ROOT, "abtest", name)  # travels to the GPU box (abtest/ is git-ignored)
     os.makedirs(out_dir, exist_ok=True)
     flags = ["-D" + d for d in defines]
 
@@ -71,8 +71,8 @@ def build_variant(name, defines, verbose=False):
     with cf.ThreadPoolExecutor(min(len(SOURCES), max(1, min(16, os.cpu_count() or 1)))) as ex:
         objs = list(ex.map(one, SOURCES))
     lib = os.path.join(out_dir, "librray_amd.so")
-    r = subprocess.run([HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", lib] + objs + ["-lz"], capture_output=True,
-                       text=True)
+    r = subprocess.run([HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", lib] + objs +
+                       ["-lz", "-L/opt/rocm/lib", "-lrccl", "-Wl,-soname,librray_amd.so"], capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed\n{r.stderr}")
     return lib

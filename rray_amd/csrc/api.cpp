@@ -267,12 +267,13 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             A.counters_zero = (c->zero_next && d == 0 && base == 0) ? frame_counters(c, c->epoch ^ 1) : nullptr;
             A.stamps = nullptr;
 #ifdef RR_STAMPS
-            // experiment builds: per-wave phase timers of level 0 of the first batch -> $RRAY_STAMPS
+            // experiment builds: per-wave phase timers of level $RRAY_STAMPS_LEVEL (0) of the first batch -> $RRAY_STAMPS
             const char* stamp_path = std::getenv("RRAY_STAMPS");
             static DBuf stamp_buf;
             const size_t stamp_bytes = (size_t)2 * (1 << 16) * 16 * sizeof(unsigned long long);
             A.stamps = nullptr;
-            if (stamp_path && d == 0 && base == 0) {
+            const int stamp_level = std::getenv("RRAY_STAMPS_LEVEL") ? std::atoi(std::getenv("RRAY_STAMPS_LEVEL")) : 0;
+            if (stamp_path && d == stamp_level && base == 0) {
                 HIPCHK(stamp_buf.ensure(stamp_bytes));
                 HIPCHK(hipMemsetAsync(stamp_buf.p, 0, stamp_bytes, st));
                 A.stamps = stamp_buf.as<unsigned long long>();

@@ -45,6 +45,11 @@ M4 load16(const double* p) {
     return m;
 }
 
+// inverse = diag(m0, m5, m10) + translation (the off-diagonal products are +-0 and drop out of the
+// reference's sums unless the whole sum is zero)
+bool is_diag12(const double* m) {
+    return m[1] == 0.0 && m[2] == 0.0 && m[4] == 0.0 && m[6] == 0.0 && m[8] == 0.0 && m[9] == 0.0;
+}
 bool is_identity12(const double* m) {
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 4; ++c)
@@ -517,7 +522,7 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
         DevNode nd{};
         std::memcpy(nd.inv, &inv12[12 * (size_t)id], sizeof(nd.inv));
         nd.kind = d.kind[id];
-        nd.flags = is_identity12(nd.inv) ? NF_IDENT : 0;
+        nd.flags = is_identity12(nd.inv) ? NF_IDENT : is_diag12(nd.inv) ? NF_DIAG : 0;
         nd.material = is_container(nd.kind) ? -1 : d.material[id];
         nd.parent = parent_node;
         nd.depth = (int32_t)anc.size();

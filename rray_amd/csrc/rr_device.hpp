@@ -15,6 +15,8 @@ namespace rr {
 enum NodeFlags : int32_t {
     NF_IDENT = 1,       // inverse transform is exactly the identity (skip the ray transform)
     NF_IN_CSG = 2,      // inside a CSG subtree: intersected only through the CSG's evaluation
+    NF_DIAG = 4,        // inverse is diagonal + translation (scale / translate objects): 3 products per
+                        // transform instead of 9 (device_core.inc xf_ray_node)
     NF_CSG_LHIT0 = 256, // bit (8 + d): for the CSG at position d of this leaf's ancestor chain,
                         // left.includes(this leaf) (csg.rs:86-88 with Object::includes semantics)
 };
