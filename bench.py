@@ -42,7 +42,14 @@ WORKLOADS = {  # name: (scene, W, H, aa, max_depth)
     "c4_teapot": ("c4_teapot.yaml", 1920, 1080, 2, 5),
     "c5_area_light": ("c5_area_light.yaml", 1920, 1080, 2, 5),
     "c1_readme": ("c1_readme.yaml", 800, 600, 1, 5),
+    # the README's example1.png scene (every shape, CSG, texture, noise): general (G = 2) kernels
+    "example1": ("../tests/golden/example1/example1.yaml", 800, 400, 3, 5),
 }
+
+
+def scene_dir(scene_file):
+    """Directory a workload's relative OBJ / texture paths resolve against (its YAML's own directory)."""
+    return os.path.dirname(os.path.normpath(os.path.join(ROOT, "scenes", scene_file)))
 SINGLE_GPU_WORKLOAD = "c2_s1024"      # BASELINE configs[1]
 MULTI_GPU_WORKLOAD = "c3_s1024_reflect"  # BASELINE configs[2]
 BLOCK = 8  # output rows per interleaved block (DESIGN.md §5)
@@ -149,7 +156,7 @@ class Session:
         self.workload = workload
         self.scene_file, self.W, self.H, self.aa, self.depth = WORKLOADS[workload]
         self.text = open(os.path.join(ROOT, "scenes", self.scene_file)).read()
-        self.scene = R.YamlScene(self.text, self.W, self.H, self.aa, obj_root=os.path.join(ROOT, "scenes"))
+        self.scene = R.YamlScene(self.text, self.W, self.H, self.aa, obj_root=scene_dir(self.scene_file))
         self.counts = scene_counts(self.scene.desc())
         self.rend = rend
         rend.upload(self.scene)
@@ -314,7 +321,8 @@ def roofline_of(sess, ktimes, stats, steps, in_region):
 def default_cpu_stride(workload):
     # bounded oracle sample (~10-30 s on 16 cores): every band for the small frames, one 8-row band in
     # every K for the big ones
-    return {"c2_s1024": 1, "c1_readme": 1, "c4_teapot": 4, "c5_area_light": 16, "c3_s1024_reflect": 16}[workload]
+    return {"c2_s1024": 1, "c1_readme": 1, "c4_teapot": 4, "c5_area_light": 16, "c3_s1024_reflect": 16,
+            "example1": 4}[workload]
 
 
 def cpu_leg(sess, args, gpu_img):
@@ -329,7 +337,7 @@ def cpu_leg(sess, args, gpu_img):
     threads = info["threads_used"]
     stride = args.cpu_stride or default_cpu_stride(sess.workload)
     W, H, aa = sess.W, sess.H, sess.aa
-    o, ocam = build_from_yaml(sess.text, W, H, aa, obj_root=os.path.join(ROOT, "scenes"))
+    o, ocam = build_from_yaml(sess.text, W, H, aa, obj_root=scene_dir(sess.scene_file))
     tc = time.perf_counter()
     canvas, _ = o.render(ocam, max_depth=sess.depth, threads=threads, band=BLOCK * aa, band_stride=stride)
     dt = time.perf_counter() - tc
@@ -466,7 +474,7 @@ def dry_run(args, world, mode, workload):
     scene_file, W0, H0, aa, depth = WORKLOADS[workload]
     W, H = 96, 54
     text = open(os.path.join(ROOT, "scenes", scene_file)).read()
-    o, cam = build_from_yaml(text, W, H, aa, obj_root=os.path.join(ROOT, "scenes"))
+    o, cam = build_from_yaml(text, W, H, aa, obj_root=scene_dir(scene_file))
     steps = args.steps or 2
     part, nparts = (rank, world) if tiles else (0, 1)
     rows = rdist.tile_rows(H, part, nparts, BLOCK)

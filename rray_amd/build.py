@@ -5,7 +5,9 @@ reference (rustc) never fuses a*b+c, and bit-parity of every discrete decision d
 """
 import concurrent.futures as cf
 import glob
+import json
 import os
+import re
 import subprocess
 import sys
 
@@ -34,6 +36,55 @@ def _deps_mtime():
     return max(os.path.getmtime(f) for f in files)
 
 
+REMARKS = ["-Rpass-analysis=kernel-resource-usage"]  # per-kernel VGPR / spill report (codegen unchanged)
+
+
+def _resources(stderr):
+    """{mangled kernel name: {"VGPRs": n, "VGPRs Spill": n, ...}} from the resource-usage remarks."""
+    out, cur = {}, None
+    for line in stderr.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = out.setdefault(m.group(1), {})
+            continue
+        m = re.search(r"remark:\s+(VGPRs|VGPRs Spill|SGPRs Spill|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]): (\d+)",
+                      line)
+        if m and cur is not None:
+            cur[m.group(1)] = int(m.group(2))
+    return out
+
+
+def cross_lane_kernel(demangled):
+    """device_core.inc cross_lane_ok: kernels whose walks read other lanes' registers (v_readlane)."""
+    m = re.search(r"rr::(shade_kernel|trace_kernel|n1n2_kernel|shadow_query_kernel)<([^>]*)>", demangled)
+    if not m:
+        return False
+    args = [a.strip() for a in m.group(2).split(",")]
+    g = int(args[0])
+    if m.group(1) == "shade_kernel":  # <G, LC, FUSED, PRE, CP, RM, AR>
+        return g < 2 and args[4] == "false" and args[6] == "false"
+    return g < 2
+
+
+def check_cross_lane(resource_files):
+    """Fail the build when a cross-lane (XL) kernel spills VGPRs: a register reloaded under a partial exec
+    mask keeps stale data in the inactive lanes, and v_readlane would return it (device_core.inc XL)."""
+    names, res = [], {}
+    for f in resource_files:
+        if os.path.exists(f):
+            res.update(json.load(open(f)))
+    names = sorted(res)
+    if not names:
+        return []
+    dem = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True).stdout.splitlines()
+    bad = [f"{d} ({res[n].get('VGPRs Spill')} VGPRs spilled)" for n, d in zip(names, dem)
+           if cross_lane_kernel(d) and res[n].get("VGPRs Spill", 0) > 0]
+    if bad:
+        raise RuntimeError("cross-lane kernels must not spill VGPRs (device_core.inc XL); move them to the "
+                           "reload path (cross_lane_ok) or lower their register use:\n  " + "\n  ".join(bad))
+    return names
+
+
 def _compile(src, deps_mtime, verbose):
     out = os.path.join(OBJ, os.path.splitext(src)[0] + ".o")
     path = os.path.join(CSRC, src)
@@ -42,11 +93,15 @@ def _compile(src, deps_mtime, verbose):
     cmd = [HIPCC] + COMMON + DEVICE + ["-c", path, "-o", out]
     if src.endswith(".cpp"):
         cmd = [HIPCC, "-x", "hip"] + COMMON + DEVICE + ["-c", path, "-o", out]
+    else:
+        cmd += REMARKS
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
+    if src.endswith(".hip"):
+        json.dump(_resources(r.stderr), open(out + ".resources.json", "w"))
     return out
 
 
@@ -86,6 +141,7 @@ def build(verbose=False, jobs=None):
     jobs = jobs or min(len(SOURCES), max(1, min(16, os.cpu_count() or 1)))
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, dm, verbose), SOURCES))
+    check_cross_lane([o + ".resources.json" for o in objs if o.endswith(".o") and os.path.exists(o + ".resources.json")])
     newest = max(os.path.getmtime(o) for o in objs)
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
         cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", LIB] + objs + ["-lz", "-L/opt/rocm/lib", "-lrccl", "-Wl,-soname,librray_amd.so"]

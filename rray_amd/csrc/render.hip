@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(256) shadow_query_kernel(DevScene S, const dou
         p = mk(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]);
         l = mk(lps[3 * i], lps[3 * i + 1], lps[3 * i + 2]);
     }
-    bool sh = shadowed<G, LC, true>(S, p, l, valid, cnt);
+    bool sh = shadowed<G, LC, true, cross_lane_ok(G, false, false)>(S, p, l, valid, cnt);
     if (valid) out[i] = sh ? 1 : 0;
     flush(cnt, counters, W_SHADOW);
 }
