@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -527,6 +528,30 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     S.general = (c->host.has_csg || c->host.has_quad) ? 1 : 0;
     const size_t lds_bytes = (size_t)S.n_nodes * sizeof(rr::DevCull) + (size_t)S.n_chunks * sizeof(rr::DevChunk);
     S.lds_culls = (lds_bytes <= (size_t)rr::RR_LDS_CULL_BYTES && !std::getenv("RRAY_GLOBAL_CULLS")) ? 1 : 0;
+    // sphere around the bounded nodes' culls (make_bundle moves far ray origins next to it)
+    {
+        double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+        bool any = false;
+        for (const rr::DevCull& cl : c->host.culls) {
+            if (!(cl.r < HUGE_VALF)) continue;
+            any = true;
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = std::min(lo[k], (double)cl.c[k] - cl.r);
+                hi[k] = std::max(hi[k], (double)cl.c[k] + cl.r);
+            }
+        }
+        S.bs_r = -1.0f;
+        if (any && std::isfinite(hi[0] - lo[0]) && std::isfinite(hi[1] - lo[1]) && std::isfinite(hi[2] - lo[2])) {
+            double r = 0.0;
+            for (int k = 0; k < 3; ++k) S.bs_c[k] = (float)(0.5 * (lo[k] + hi[k]));
+            for (const rr::DevCull& cl : c->host.culls) {
+                if (!(cl.r < HUGE_VALF)) continue;
+                const double dx = cl.c[0] - S.bs_c[0], dy = cl.c[1] - S.bs_c[1], dz = cl.c[2] - S.bs_c[2];
+                r = std::max(r, std::sqrt(dx * dx + dy * dy + dz * dz) + cl.r);
+            }
+            if (r < 1e30) S.bs_r = (float)r;
+        }
+    }
     c->has_scene = true;
     return RR_OK;
 }

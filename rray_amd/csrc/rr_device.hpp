@@ -143,6 +143,8 @@ struct DevScene {
     int32_t lds_culls;        // culls + chunks staged in LDS per workgroup (fits in RR_LDS_CULL_BYTES)
     int32_t complex_patterns; // some pattern is Gradient / Blend / Perturbed / Noise / Texture
     int32_t pad3;
+    float bs_c[3], bs_r;      // sphere around every bounded node's cull (bs_r < 0: none); rays whose origin
+                              // lies far outside it are culled from a point nearer to it (make_bundle)
 };
 // Node culls (16 B each) and chunk records (32 B each) are copied into LDS by every walking
 // workgroup when together they fit in this many bytes.  Small scenes gain from it (C5 2.5 %, C1
