@@ -169,13 +169,17 @@ unsigned long long* frame_counters(rr_ctx* c, int k) {
 // children (k), so level d holds at most nb * k^d events.  The levels are launched for that capacity
 // and read their live counts from HBM (no host round trip between levels).
 struct LevelPlan {
-    int64_t cap[RR_MAX_DEPTH + 1];  // capacity per level
+    int64_t cap[RR_MAX_DEPTH + 1];  // capacity per level (array size; segmented: nseg * seg_cap)
+    int64_t seg_cap[RR_MAX_DEPTH + 1];  // segmented (fused) levels >= 1: capacity of each of RR_NSEG segments
     int levels;                     // levels launched (depth + 1, or 1 without secondary rays)
     int64_t ev_cap[2];              // ev_a (odd levels), ev_b (even levels >= 2)
     int64_t max_cap;
     size_t bytes;
 };
-LevelPlan plan_levels(int64_t nb, int k, int max_depth, bool ext) {
+// fused: levels >= 1 in RR_NSEG segments (wavefront.hpp); level 0's block b fills segment b % RR_NSEG
+// of level 1, so a segment holds at most ceil(blocks / RR_NSEG) * 256 * k events, and a segment of
+// level d feeds only the same segment of level d + 1
+LevelPlan plan_levels(int64_t nb, int k, int max_depth, bool ext, bool fused = false) {
     LevelPlan p{};
     int64_t w = nb;
     for (int d = 0; d <= max_depth; ++d) {
@@ -185,7 +189,13 @@ LevelPlan plan_levels(int64_t nb, int k, int max_depth, bool ext) {
         const bool kids = d < max_depth && k > 0;
         if (!kids) break;
         p.bytes += (size_t)w * (sizeof(rr::CombRec) + (ext ? sizeof(rr::CombExt) : 0) + sizeof(int32_t));
-        w *= k;
+        if (fused) {
+            p.seg_cap[d + 1] = d == 0 ? (((nb + 255) / 256 + rr::RR_NSEG - 1) / rr::RR_NSEG) * 256 * k : p.seg_cap[d] * k;
+            p.seg_cap[d + 1] = (p.seg_cap[d + 1] + 255) / 256 * 256;
+            w = rr::RR_NSEG * p.seg_cap[d + 1];
+        } else {
+            w *= k;
+        }
         int64_t& e = p.ev_cap[d % 2];  // level d+1 lands in ev_a when d is even
         e = std::max(e, w);
     }
@@ -198,17 +208,18 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
                void* avg = nullptr, int32_t avg_f32 = 0) {
     const int k = c->host.max_children;
     const bool ext = c->host.has_transparent != 0;
+    const bool fused = rr::fused_levels(c->S);
     // batch: at most c->batch camera samples, shrunk (power-of-two steps, tile-aligned) until the
     // worst-case queues fit the context's budget and every event index fits in int32
     int64_t B = std::max<int64_t>(64, std::min<int64_t>(c->batch, total));
     for (;;) {
-        const LevelPlan p = plan_levels(B, k, max_depth, ext);
+        const LevelPlan p = plan_levels(B, k, max_depth, ext, fused);
         const int64_t last = p.cap[p.levels - 1];
         if (B <= 4096 || (p.bytes <= c->queue_budget && last < ((int64_t)1 << 31) && p.max_cap < ((int64_t)1 << 31)))
             break;
         B = std::max<int64_t>(4096, (B / 2) & ~(int64_t)63);
     }
-    const LevelPlan P = plan_levels(B, k, max_depth, ext);
+    const LevelPlan P = plan_levels(B, k, max_depth, ext, fused);
     if (P.max_cap >= ((int64_t)1 << 31)) return fail(RR_E_LIMIT, "recursion queues exceed 2^31 events (lower max_depth)");
     if ((int)c->comb.size() < P.levels) {
         c->comb.resize(P.levels);
@@ -228,7 +239,7 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
     unsigned int* lc = c->lcount.as<unsigned int>();
     for (int64_t base = 0; base < total; base += B) {
         const int64_t nb = std::min(B, total - base);
-        const LevelPlan p = plan_levels(nb, k, max_depth, ext);
+        const LevelPlan p = plan_levels(nb, k, max_depth, ext, fused);
         // per-level queue counters [level][LC_*], zeroed once per batch (appends, pending, n1/n2 lists)
         if (p.levels > 1 || ext)
             HIPCHK(hipMemsetAsync(lc, 0, (size_t)p.levels * rr::LC_COUNT * sizeof(unsigned int), st));
@@ -246,6 +257,12 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             A.rem = max_depth - d;
             A.n = p.cap[d];
             A.n_dev = d > 0 ? lc + (d - 1) * rr::LC_COUNT + rr::LC_CHILDREN : nullptr;
+            A.nseg = fused && d > 0 ? rr::RR_NSEG : 1;
+            A.nseg_out = fused ? rr::RR_NSEG : 1;
+            A.seg_cap = fused && d > 0 ? p.seg_cap[d] : 0;
+            A.seg_cap_out = fused && children_possible ? p.seg_cap[d + 1] : 0;
+            A.seg_count = lc + d * rr::LC_COUNT + rr::LC_SEG0;
+            A.seg_out_count = children_possible ? lc + (d + 1) * rr::LC_COUNT + rr::LC_SEG0 : nullptr;
             // level d reads ev_b when d is even (d >= 2), ev_a when odd; writes the other one
             A.ev = d == 0 ? nullptr : (d % 2 ? c->ev_a : c->ev_b).as<rr::Event>();
             A.hit = c->hit.as<rr::HitRec>();
@@ -278,6 +295,7 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
                 HIPCHK(stamp_buf.ensure(stamp_bytes));
                 HIPCHK(hipMemsetAsync(stamp_buf.p, 0, stamp_bytes, st));
                 A.stamps = stamp_buf.as<unsigned long long>();
+                A.stamp_stride = std::getenv("RRAY_STAMPS_STRIDE") ? std::max(1, std::atoi(std::getenv("RRAY_STAMPS_STRIDE"))) : 1;
             }
 #endif
             HIPCHK(rr::launch_level(c->S, A, st, c->profile ? &c->prof : nullptr));

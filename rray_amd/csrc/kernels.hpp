@@ -25,6 +25,13 @@ struct LevelArgs {
     int32_t level, rem;      // level d and `remaining` = max_depth - d
     int64_t n;               // events at this level (n_dev == null) or this level's capacity (the grid)
     const unsigned int* n_dev;  // level >= 1: the live event count, written by the previous level's appends
+    // segmented queues (fused levels, wavefront.hpp): this level's events are seg_count[s] events at
+    // s * seg_cap (nseg > 1; level 0 has one segment), its children go to segment blockIdx % nseg_out of
+    // the next level at s * seg_cap_out, counted in seg_out_count[s]
+    int32_t nseg, nseg_out;
+    int64_t seg_cap, seg_cap_out;
+    const unsigned int* seg_count;
+    unsigned int* seg_out_count;
     const Event* ev;         // level >= 1 input queue
     HitRec* hit;
     double* n12;
@@ -45,6 +52,7 @@ struct LevelArgs {
     unsigned long long* counters;  // C_* totals
     unsigned long long* counters_zero;  // the next frame's counter buffer, zeroed by this frame's kernels (or null)
     unsigned long long* stamps;    // RR_STAMPS experiment builds only: per-wave phase timers (else null)
+    int64_t stamp_stride;          // RR_STAMPS: every stamp_stride-th wave is recorded ($RRAY_STAMPS_STRIDE)
 };
 
 struct CombArgs {

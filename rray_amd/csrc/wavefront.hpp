@@ -53,7 +53,14 @@ struct alignas(16) ChainRec {
 static_assert(sizeof(ChainRec) == 48 && sizeof(ChainRec) <= sizeof(CombRec), "ChainRec layout");
 enum { CF_HIT = 1, CF_REFRACT_CHILD = 2 };
 
-// per-level device counters
-enum { LC_CHILDREN = 0, LC_PENDING, LC_N1N2, LC_COUNT };
+// per-level device counters.  Fused levels (no transparency) queue their children in RR_NSEG segments
+// (block b appends to segment b % RR_NSEG with one atomic per wave, no workgroup barrier; the next
+// level's block b reads segment b % RR_NSEG — blocks are dealt to the XCDs round-robin, so a segment's
+// producer and consumer run on the same XCD); LC_SEG0 + s counts segment s of the level.
+#ifndef RR_NSEG_N
+#define RR_NSEG_N 1024
+#endif
+constexpr int RR_NSEG = RR_NSEG_N;
+enum { LC_CHILDREN = 0, LC_PENDING, LC_N1N2, LC_SEG0, LC_COUNT = LC_SEG0 + RR_NSEG };
 
 }  // namespace rr
