@@ -402,17 +402,25 @@ def gpu_bench(args, world, mode, workload):
     value = frames_per_step * samples_per_frame * steps / elapsed / 1e6
     roofline = roofline_of(sess, ktimes, stats, steps, in_region)
 
-    # tiles: the gathered frame must be bit-identical to one part rendering the whole frame (§8(e))
-    identity = None
+    # tiles: the gathered frame must be bit-identical to one part rendering the whole frame (§8(e)); rank 0
+    # also times that single-GPU render of the same workload (the other ranks wait at the barrier), so the
+    # line carries its own 1-GPU point
+    identity = single = None
     if sess.multi:
         gathered = sess.frame() if rank == 0 else None
         if rank == 0:
             one = R.Renderer(local)  # a plain single-device context renders the whole frame as one part
             one.upload(sess.scene)
             full = one.render(sess.cam, aa=sess.aa, max_depth=sess.depth)["avg"]
-            one.close()
             identity = {"bit_identical_to_1_part": bool(np.array_equal(gathered, full)),
                         "max_abs_diff": float(np.max(np.abs(gathered - full)))}
+            a = Session(R, workload, dev, local, 0, 1, True, False, one)
+            k1 = max(2, min(steps, 5))
+            a_el, _, _, _, _ = timed_loop(a, k1, 1, False, dist, torch)
+            single = {"n_gpus": 1, "steps": k1, "ms_per_step": round(a_el / k1 * 1e3, 4),
+                      "value": round(a.W * a.H * a.aa * a.aa * k1 / a_el / 1e6, 3),
+                      "note": "the same frame rendered as one part on rank 0's GPU after the timed region"}
+            one.close()
         dist.barrier()
 
     cpu = parity = anchor = None
@@ -443,7 +451,8 @@ def gpu_bench(args, world, mode, workload):
                            "objects": sess.counts["objects"], "frames_per_step": frames_per_step,
                            "parallelism": par},
                 "roofline": roofline, "cpu_baseline": cpu, "parity_sample": parity,
-                "tile_identity": identity, "scaling_anchor": anchor,
+                "tile_identity": identity, "scaling_anchor": anchor, "single_gpu": single,
+                "speedup_vs_single_gpu": round(value / single["value"], 3) if single else None,
                 "kernels_ms_per_step": {k: round(v[0] / steps, 4) for k, v in ktimes.items() if v[1]},
                 "host_enqueue_ms_per_step": round(t_enq / steps * 1e3, 4),
                 "stats_last_step": {k: stats[k] for k in ("rays", "shadow_rays", "shade_events", "n1n2_scans",
