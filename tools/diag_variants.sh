@@ -1,5 +1,5 @@
 #!/bin/bash
-# Parity of a few scenes under experiment builds (rray_amd/_exp/<name>, see build.build_variant),
+# Parity of a few scenes under experiment builds (abtest/<name>, see build.build_variant),
 # each run twice to expose run-to-run differences.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

@@ -1,4 +1,4 @@
-"""Summarise an RR_STAMPS dump (rray_amd/_exp/stamps, $RRAY_STAMPS) of the fused level-0 shade kernel:
+"""Summarise an RR_STAMPS dump (abtest/stamps, $RRAY_STAMPS; tools/stamps_run.sh) of the fused level-0 shade kernel:
 mean s_memtime cycles per wave between phase marks.  Region 1 = shade kernel marks, region 0 =
 the shadow walk and extra marks (render.hip, RR_STAMPX)."""
 import sys
