@@ -527,6 +527,15 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     S.culls = c->culls.as<rr::DevCull>();
     S.chunks = c->chunks.as<rr::DevChunk>();
     S.n_chunks = (int32_t)c->host.chunks.size();
+    S.n_free = 0;
+    for (int k = S.n_chunks - 1; k >= 0; --k) {  // lone unbounded top-level leaves at the end of the order
+        const rr::DevChunk& ch = c->host.chunks[k];
+        const rr::DevNode& nd = c->host.nodes[ch.start];
+        if (ch.count != 1 || ch.cull.r < HUGE_VALF || nd.parent != -1 || rr::is_container(nd.kind) ||
+            ch.start != (int32_t)c->host.nodes.size() - 1 - S.n_free)
+            break;
+        ++S.n_free;
+    }
     S.nodes = c->nodes.as<rr::DevNode>();
     S.groups = c->groups.as<rr::DevGroup>();
     S.shapes = c->shapes.as<rr::DevShape>();
