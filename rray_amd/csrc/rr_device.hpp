@@ -143,7 +143,7 @@ struct DevScene {
     int32_t lds_culls;        // culls + chunks staged in LDS per workgroup (fits in RR_LDS_CULL_BYTES)
     int32_t complex_patterns; // some pattern is Gradient / Blend / Perturbed / Noise / Texture
     int32_t n_free;           // trailing chunks holding one unbounded top-level leaf each (planes): the
-                              // last n_free nodes, tested without culling before the chunk passes (G = 0)
+                              // last n_free nodes, tested without culling before the chunk passes
     float bs_c[3], bs_r;      // sphere around every bounded node's cull (bs_r < 0: none); rays whose origin
                               // lies far outside it are culled from a point nearer to it (make_bundle)
 };
