@@ -275,16 +275,29 @@ def roofline_of(sess, ktimes, stats, steps, in_region):
     launches_per_step = dom_n / steps
     # flops of one step / (this kernel's time per step) == per-launch flops / average launch duration
     achieved = flops / (dom_ms / steps / 1e3) / 1e12 if dom_ms > 0 else 0.0
-    traffic, entry = None, {}
+    # HBM traffic and VALU busy come from a RECORDED rocprofv3 PMC session (profiles/pmc_<workload>.json; PMC
+    # counters need their own profiler runs).  They are reported only when that session measured this very
+    # build (same source digest); otherwise null, with the recorded values kept under "recorded_profile".
+    from rray_amd.build import source_digest
+
+    traffic, entry, rec = None, {}, {"status": "none"}
     pmc = os.path.join(ROOT, "profiles", f"pmc_{sess.workload}.json")
     if os.path.exists(pmc):
         try:
             per_kernel = json.load(open(pmc))
             # the fused trace+shade launch is the shade_kernel<..., FUSED> instantiation in rocprof's naming
             entry = per_kernel.get(dom) or (per_kernel.get("shade") if dom == "trace_shade" else None) or {}
-            traffic = entry.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
-            traffic, entry = None, {}
+            entry = {}
+        here = source_digest()
+        current = bool(entry) and entry.get("src_digest") == here
+        rec = {"status": "current" if current else "stale", "profile": entry.get("profile"),
+               "profile_src_digest": entry.get("src_digest"), "this_build_src_digest": here,
+               "hbm_bytes_per_launch": entry.get("hbm_bytes_per_launch"), "valu_busy_frac": entry.get("valu_busy_frac")}
+        if current:
+            traffic = entry.get("hbm_bytes_per_launch")
+        else:
+            entry = {}
     c = sess.counts
     # SURVEY §8(d) full-scan model for the same rays: what the reference's algorithm would execute
     per_ray = FLOPS["sphere"] * c["sphere"] + FLOPS["plane"] * c["plane"] + FLOPS["group"] * c["group"] + FLOPS["tri"] * c["tri"]
@@ -305,6 +318,9 @@ def roofline_of(sess, ktimes, stats, steps, in_region):
                                      "flops_per_step": ref_flops,
                                      "model": "SURVEY §8(d) full scan (every ray tests every primitive; "
                                               "triangles counted as if their group box were hit)"},
+            "traffic_source": "recorded rocprofv3 PMC session of this build (2*FETCH_SIZE + WRITE_SIZE per launch)"
+                              if traffic is not None else "no PMC session of this build recorded: null",
+            "recorded_profile": rec,
             "valu_busy": {"frac": entry.get("valu_busy_frac"), "rocprof_kernel_ms":
                           (entry["rocprof_avg_ns"] / 1e6 if entry.get("rocprof_avg_ns") else None),
                           "source": entry.get("profile"),
@@ -493,6 +509,8 @@ def dry_run(args, world, mode, workload):
         avg = o.aa_average(np.nan_to_num(canvas), aa)
         out[: len(rows)] = torch.from_numpy(avg[rows])
 
+    # multi.cpp's layout: f64 tiles padded to part 0's row count, gathered back to back on rank 0 and
+    # un-interleaved by the library's rr_unshuffle_host (the device kernel's index arithmetic)
     pipe = rdist.FramePipeline(H, W, 3, torch.float64, torch.device("cpu"), block=BLOCK) if (tiles and distributed) \
         else None
     t0 = time.perf_counter()
@@ -515,9 +533,16 @@ def dry_run(args, world, mode, workload):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     identity = None
+    if pipe is not None:  # one more frame through the library's host un-interleave (rr_unshuffle_host)
+        tile = torch.zeros((rdist.max_tile_rows(H, world, BLOCK), W, 3), dtype=torch.float64)
+        render_tile(tile)
+        via_lib = rdist.gather_frame(tile, H, BLOCK)
     if rank == 0 and pipe is not None:
         full, _ = o.render(cam, max_depth=depth, threads=2)
-        identity = {"bit_identical_to_1_part": bool(np.array_equal(pipe.frame.numpy(), o.aa_average(full, aa)))}
+        ref = o.aa_average(np.nan_to_num(full), aa)
+        identity = {"bit_identical_to_1_part": bool(np.array_equal(pipe.frame.numpy(), ref)),
+                    "rr_unshuffle_host_bit_identical": bool(np.array_equal(via_lib.numpy(), ref)),
+                    "layout": "multi.cpp: padded f64 tiles back to back (ncclGather layout), library un-interleave"}
     if rank == 0:
         frames_per_step = world if not tiles else 1
         line = {"metric": METRIC, "value": round(frames_per_step * W * H * aa * aa * steps / elapsed / 1e6, 6),

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 6
+#define RR_ABI_VERSION 7
 
 /* error codes */
 #define RR_OK 0
@@ -56,7 +56,12 @@ enum { RR_LIGHT_POINT = 0, RR_LIGHT_AREA = 1 };
 
 #define RR_MAX_DEPTH 8          /* max `remaining` (render uses 5, camera.rs:113) */
 #define RR_MAX_GROUP_DEPTH 6    /* nested group levels */
-#define RR_MAX_AREA_LEVEL 1024  /* area light `level` (level^2 jittered samples per shading event) */
+#define RR_MAX_AREA_LEVEL 1024  /* area light `level` (level^2 jittered samples per shading event; the
+                                   reference takes any usize, scene_builder_yaml.rs:137).  Bound by the
+                                   kernels' cell arithmetic: (col + u) / level is the proven shared-divisor
+                                   quotient (tests/test_division.py, every level 1..1024) and the cell index
+                                   s < level^2 <= 2^20 fits the jitter key's 20-bit field.  The YAML front-end
+                                   and rr_scene_upload both refuse larger levels (RR_E_LIMIT / RR_E_SCENE). */
 #define RR_MAX_PATTERN_DEPTH 8  /* nested pattern levels */
 #define RR_MAX_CSG_ENTRIES 32   /* intersections one CSG subtree can produce for one ray */
 #define RR_MAX_OCTAVES 64       /* octave_perlin octaves (noise.rs:11-29) */
@@ -186,6 +191,17 @@ int rr_rccl_unique_id(uint8_t* out, int32_t n_bytes);
 int rr_create_rank(int device, int nranks, int rank, const uint8_t* unique_id, rr_ctx** out);
 /* nranks in the group, this context's first global rank, devices this context drives (1/0/1 for rr_create) */
 int rr_context_info(const rr_ctx* ctx, int32_t* nranks, int32_t* rank, int32_t* ndevices);
+/* ABI 7: nparts VIRTUAL ranks on one device — the N > 1 path of a real group (per-part contexts and
+ * streams, padded tiles, the receive buffer in ncclGather's layout, double buffering, the un-interleave
+ * kernel) with the transfer replaced by device-local copies.  For exercising / testing the multi-GPU
+ * frame assembly on one GPU; images are bit-identical to one part's. */
+int rr_create_virtual(int device, int nparts, rr_ctx** out);
+/* ABI 7: host restatement of the root's un-interleave (the same index arithmetic as the device kernel):
+ * gathered = nparts tiles back to back, each rr_part_rows(height, 0, nparts, block_rows, NULL) rows of
+ * width*3 doubles (part p's rows in increasing y, padded) -> frame = height rows in frame order.  No
+ * device needed (CPU rehearsals of the N > 1 path use it). */
+int rr_unshuffle_host(const double* gathered, double* frame, int64_t width, int64_t height, int32_t nparts,
+                      int32_t block_rows);
 /* Whole frame -> d_frame (W*H*3 doubles on rank 0's device; ignored on other ranks), enqueued after
  * the work already on `hip_stream` (NULL: no ordering with the caller) and completed in its order;
  * not synchronised.  Collective: every rank calls it for every frame.  Tiles are double-buffered, so

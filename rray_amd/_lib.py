@@ -7,8 +7,14 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "librray_amd.so")
-if os.environ.get("RRAY_LIB"):  # experiment builds (build.build_variant); the default is the in-tree product
-    LIB_PATH = os.environ["RRAY_LIB"]
+# Experiment builds (build.build_variant -> abtest/<name>/librray_amd.so) stand in for the product only
+# when explicitly marked as an experiment run (RRAY_EXPERIMENT=1) and only from the repo's abtest/ tree;
+# the product path always loads the in-tree library.
+if os.environ.get("RRAY_LIB") and os.environ.get("RRAY_EXPERIMENT") == "1":
+    _cand = os.path.realpath(os.environ["RRAY_LIB"])
+    if not _cand.startswith(os.path.join(os.path.dirname(HERE), "abtest") + os.sep):
+        raise RuntimeError(f"RRAY_LIB={_cand}: experiment libraries must live under abtest/")
+    LIB_PATH = _cand
 HEADER = os.path.join(os.path.dirname(HERE), "include", "rray", "rray.h")
 
 RR_OK = 0
@@ -69,7 +75,8 @@ EXPORTS = ["rr_abi_version", "rr_last_error", "rr_device_count", "rr_create", "r
            "rr_last_stats", "rr_color_at",
            "rr_is_shadowed", "rr_scene_inspect", "rr_scene_from_yaml", "rr_scene_desc_of", "rr_scene_free", "rr_quantize",
            "rr_write_png", "rr_render_scene_from_file", "rr_render_scene_from_file_devices", "rr_create_multi",
-           "rr_rccl_unique_id", "rr_create_rank", "rr_context_info", "rr_render_gather_device"]
+           "rr_rccl_unique_id", "rr_create_rank", "rr_context_info", "rr_render_gather_device", "rr_create_virtual",
+           "rr_unshuffle_host"]
 RCCL_ID_BYTES = 128
 
 _lib = None
@@ -121,6 +128,8 @@ def lib():
     L.rr_rccl_unique_id.argtypes = [C.POINTER(C.c_uint8), C.c_int32]
     L.rr_create_rank.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.POINTER(C.c_void_p)]
     L.rr_context_info.argtypes = [C.c_void_p, _I, _I, _I]
+    L.rr_create_virtual.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+    L.rr_unshuffle_host.argtypes = [_D, _D, C.c_int64, C.c_int64, C.c_int32, C.c_int32]
     L.rr_render_gather_device.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(RenderOpts), C.c_void_p,
                                           C.c_void_p]
     _lib = L

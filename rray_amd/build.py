@@ -29,6 +29,21 @@ LEVEL_UNITS = [f"render_levels_g{g}_{lc}.hip" for g in (2, 1, 0) for lc in ("lds
 SOURCES = LEVEL_UNITS + ["render.hip", "api.cpp", "multi.cpp", "flatten.cpp", "frontend.cpp", "yaml.cpp", "png.cpp"]
 
 
+def source_digest():
+    """sha256 of the product sources (kernels, host library, header, this build script): identifies
+    which build a recorded profile (profiles/pmc_*.json) was measured on."""
+    import hashlib
+
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(CSRC, "*")) + [os.path.join(ROOT, "include", "rray", "rray.h"),
+                                                          os.path.abspath(__file__)])
+    for f in files:
+        if os.path.isfile(f):
+            h.update(os.path.basename(f).encode())
+            h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def _deps_mtime():
     files = glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(os.path.join(CSRC, "*.inc"))
     files += glob.glob(os.path.join(ROOT, "include", "rray", "*.h"))

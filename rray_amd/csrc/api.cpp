@@ -11,9 +11,11 @@
 #include <vector>
 
 #include "../../include/rray/rray.h"
+#include "device_guard.hpp"
 #include "flatten.hpp"
 #include "kernels.hpp"
 #include "multi.hpp"
+#include "partition.hpp"
 #include "rr_math.hpp"
 
 namespace {
@@ -132,13 +134,6 @@ rr::DevCamera dev_camera(const rr_camera* c) {
     for (int r = 0; r < 4; ++r)  // camera.rs:86 with the kernel's operation order (no contraction)
         d.origin[r] = d.inv[4 * r] * 0.0 + d.inv[4 * r + 1] * 0.0 + d.inv[4 * r + 2] * 0.0 + d.inv[4 * r + 3] * 1.0;
     return d;
-}
-
-int64_t part_rows_count(int64_t height, int32_t part, int32_t nparts, int32_t block) {
-    int64_t n = 0;
-    for (int64_t b0 = (int64_t)part * block; b0 < height; b0 += (int64_t)nparts * block)
-        n += std::min<int64_t>(block, height - b0);
-    return n;
 }
 
 // Runs the wavefront levels for `total` level-0 events; level-0 rays come from the camera or from
@@ -394,6 +389,23 @@ int finish_stats(rr_ctx* c) {
 
 }  // namespace
 
+namespace rr {
+// Every check rr_render_device makes before it enqueues anything (the multi-device group validates all
+// of its parts with it first, so a bad argument never leaves peers waiting in a collective).
+int render_validate(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o) {
+    if (!c) return fail(RR_E_ARG, "null context");
+    if (c->group) return fail(RR_E_ARG, "multi-device context: use rr_render_gather_device or rr_render");
+    if (!c->has_scene) return fail(RR_E_ARG, "no scene uploaded");
+    int rc = check_opts(cam, o);
+    if (rc != RR_OK) return rc;
+    const int32_t block = o->block_rows > 0 ? o->block_rows : 8;
+    const int64_t rows = part_rows_count(cam->vsize / o->aa, o->part, o->nparts, block);
+    if (rows * o->aa * cam->hsize >= ((int64_t)1 << 31))
+        return fail(RR_E_LIMIT, "a part must hold fewer than 2^31 samples (use more parts)");
+    return RR_OK;
+}
+}  // namespace rr
+
 extern "C" {
 
 int32_t rr_abi_version(void) { return RR_ABI_VERSION; }
@@ -408,6 +420,7 @@ int rr_device_count(int* out) {
 }
 
 int rr_create(int device, rr_ctx** out) {
+    rr::DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!out) return fail(RR_E_ARG, "null out");
     *out = nullptr;
     int n = 0;
@@ -443,6 +456,7 @@ int rr_create(int device, rr_ctx** out) {
 }
 
 int rr_create_multi(int n, const int* device_ids, rr_ctx** out) {
+    rr::DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!out) return fail(RR_E_ARG, "null out");
     *out = nullptr;
     rr_group* g = nullptr;
@@ -455,6 +469,7 @@ int rr_create_multi(int n, const int* device_ids, rr_ctx** out) {
 }
 
 int rr_create_rank(int device, int nranks, int rank, const uint8_t* unique_id, rr_ctx** out) {
+    rr::DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!out) return fail(RR_E_ARG, "null out");
     *out = nullptr;
     rr_group* g = nullptr;
@@ -476,6 +491,7 @@ int rr_context_info(const rr_ctx* c, int32_t* nranks, int32_t* rank, int32_t* nd
 }
 
 void rr_destroy(rr_ctx* c) {
+    rr::DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!c) return;
     if (c->group) {
         rr::group_destroy(c->group);
@@ -501,6 +517,7 @@ void rr_destroy(rr_ctx* c) {
 }
 
 int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
+    rr::DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!c || !d) return fail(RR_E_ARG, "null context/descriptor");
     if (c->group) return rr::group_upload(c->group, d);
     std::string err;
@@ -639,29 +656,50 @@ int rr_camera_new(int64_t hsize, int64_t vsize, double fov, const double transfo
 
 int64_t rr_part_rows(int64_t height, int32_t part, int32_t nparts, int32_t block, int64_t* rows_out) {
     if (nparts < 1 || part < 0 || part >= nparts || block < 1 || height < 0) return fail(RR_E_ARG, "bad partition");
-    int64_t n = 0;
-    for (int64_t b0 = (int64_t)part * block; b0 < height; b0 += (int64_t)nparts * block)
-        for (int64_t y = b0; y < std::min<int64_t>(b0 + block, height); ++y) {
-            if (rows_out) rows_out[n] = y;
-            ++n;
-        }
+    const int64_t n = rr::part_rows_count(height, part, nparts, block);
+    if (rows_out) {
+        int64_t k = 0;
+        for (int64_t b0 = (int64_t)part * block; b0 < height; b0 += (int64_t)nparts * block)
+            for (int64_t y = b0; y < std::min<int64_t>(b0 + block, height); ++y) rows_out[k++] = y;
+    }
     return n;
+}
+
+int rr_unshuffle_host(const double* gathered, double* frame, int64_t width, int64_t height, int32_t nparts,
+                      int32_t block) {
+    if (!gathered || !frame || width < 0 || height < 0 || nparts < 1 || block < 1)
+        return fail(RR_E_ARG, "rr_unshuffle_host: bad arguments");
+    const int64_t tile_rows = rr::gather_tile_rows(height, nparts, block), row = width * 3;
+    for (int64_t y = 0; y < height; ++y)
+        std::memcpy(frame + y * row, gathered + rr::gathered_row_of(y, nparts, block, tile_rows) * row,
+                    (size_t)row * sizeof(double));
+    return RR_OK;
+}
+
+int rr_create_virtual(int device, int nparts, rr_ctx** out) {
+    rr::DeviceGuard device_guard;
+    if (!out) return fail(RR_E_ARG, "null out");
+    *out = nullptr;
+    rr_group* g = nullptr;
+    int rc = rr::group_create_virtual(device, nparts, &g);
+    if (rc != RR_OK) return rc;
+    rr_ctx* c = new rr_ctx();
+    c->group = g;
+    *out = c;
+    return RR_OK;
 }
 
 int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, void* d_canvas, void* d_avg,
                      void* hip_stream) {
-    if (!c) return fail(RR_E_ARG, "null context");
-    if (c->group) return fail(RR_E_ARG, "multi-device context: use rr_render_gather_device or rr_render");
-    if (!c->has_scene) return fail(RR_E_ARG, "no scene uploaded");
-    int rc = check_opts(cam, o);
+    rr::DeviceGuard device_guard;  // the caller's current device is restored on return
+    int rc = rr::render_validate(c, cam, o);
     if (rc != RR_OK) return rc;
     HIPCHK(hipSetDevice(c->device));
     const int32_t block = o->block_rows > 0 ? o->block_rows : 8;
     const int64_t H = cam->vsize / o->aa, W = cam->hsize / o->aa;
-    const int64_t rows = part_rows_count(H, o->part, o->nparts, block);
+    const int64_t rows = rr::part_rows_count(H, o->part, o->nparts, block);
     const int64_t local_rows = rows * o->aa;
     const int64_t total = local_rows * cam->hsize;
-    if (total >= ((int64_t)1 << 31)) return fail(RR_E_LIMIT, "a part must hold fewer than 2^31 samples (use more parts)");
     // Everything is enqueued on the caller's stream (no cross-stream events per call: a HIP event
     // handoff between streams costs host time every frame).  The context's workspace is reused, so
     // a render on a different stream than the previous one first waits for that one.
@@ -710,6 +748,7 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
 }
 
 int rr_render_gather_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, void* d_frame, void* hip_stream) {
+    rr::DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!c) return fail(RR_E_ARG, "null context");
     if (c->group) return rr::group_render_gather(c->group, cam, o, d_frame, hip_stream);
     if (o && (o->nparts != 1 || o->part != 0)) return fail(RR_E_ARG, "rr_render_gather_device renders the whole frame");
@@ -720,6 +759,7 @@ int rr_render_gather_device(rr_ctx* c, const rr_camera* cam, const rr_render_opt
 }
 
 int rr_kernel_profile(rr_ctx* c, int enable) {
+    rr::DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!c) return fail(RR_E_ARG, "null context");
     if (c->group) return rr_kernel_profile(rr::group_local(c->group, 0), enable);
     HIPCHK(sync_ctx(c));
@@ -734,6 +774,7 @@ int rr_kernel_profile(rr_ctx* c, int enable) {
 }
 
 int rr_kernel_times(rr_ctx* c, double* ms, uint64_t* launches, int32_t n) {
+    rr::DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!c) return fail(RR_E_ARG, "null context");
     if (c->group) return rr_kernel_times(rr::group_local(c->group, 0), ms, launches, n);
     HIPCHK(sync_ctx(c));
@@ -747,6 +788,7 @@ int rr_kernel_times(rr_ctx* c, double* ms, uint64_t* launches, int32_t n) {
 }
 
 int rr_last_stats(rr_ctx* c, rr_stats* s) {
+    rr::DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!c || !s) return fail(RR_E_ARG, "null argument");
     if (c->group) return rr::group_last_stats(c->group, s);
     uint64_t samples = c->last.samples;
@@ -759,13 +801,14 @@ int rr_last_stats(rr_ctx* c, rr_stats* s) {
 
 int rr_render(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, double* out_canvas, double* out_avg,
               rr_stats* stats) {
+    rr::DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!c) return fail(RR_E_ARG, "null context");
     if (c->group) return rr::group_render(c->group, cam, o, out_canvas, out_avg, stats);
     int rc = check_opts(cam, o);
     if (rc != RR_OK) return rc;
     const int32_t block = o->block_rows > 0 ? o->block_rows : 8;
     const int64_t H = cam->vsize / o->aa, W = cam->hsize / o->aa;
-    const int64_t rows = part_rows_count(H, o->part, o->nparts, block);
+    const int64_t rows = rr::part_rows_count(H, o->part, o->nparts, block);
     const int64_t total = rows * o->aa * cam->hsize;
     HIPCHK(hipSetDevice(c->device));
     const bool want_avg = (o->flags & RR_OUT_AVG) && out_avg;
@@ -788,6 +831,7 @@ int rr_render(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, double* 
 
 int rr_color_at(rr_ctx* c, int64_t n, const double* origins, const double* directions, int32_t remaining,
                 uint64_t seed, int32_t jitter_mode, double* out_rgb) {
+    rr::DeviceGuard device_guard;  // the caller's current device is restored on return
     if (c && c->group) return rr_color_at(rr::group_local(c->group, 0), n, origins, directions, remaining, seed, jitter_mode, out_rgb);
     if (!c || (n > 0 && (!origins || !directions || !out_rgb))) return fail(RR_E_ARG, "null argument");
     if (!c->has_scene) return fail(RR_E_ARG, "no scene uploaded");
@@ -820,13 +864,17 @@ int rr_color_at(rr_ctx* c, int64_t n, const double* origins, const double* direc
     c->epoch = saved_epoch;
     if (rc != RR_OK) return rc;
     HIPCHK(hipMemcpyAsync(out_rgb, c->qout.p, n * 3 * sizeof(double), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpy(c->h_counters, frame_counters(c, 2), kCounterBytes, hipMemcpyDeviceToHost));
+    // the counters on the same (non-blocking) stream, then wait: out_rgb and the counters are both
+    // complete on return, whatever kind of host memory the caller passed
+    HIPCHK(hipMemcpyAsync(c->h_counters, frame_counters(c, 2), kCounterBytes, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
     rr_stats q;
     collect_stats(c, &q);
     return q.nan_rays ? nan_fail(q.nan_rays) : RR_OK;
 }
 
 int rr_is_shadowed(rr_ctx* c, int64_t n, const double* points, const double* light_positions, int32_t* out) {
+    rr::DeviceGuard device_guard;  // the caller's current device is restored on return
     if (c && c->group) return rr_is_shadowed(rr::group_local(c->group, 0), n, points, light_positions, out);
     if (!c || (n > 0 && (!points || !light_positions || !out))) return fail(RR_E_ARG, "null argument");
     if (!c->has_scene) return fail(RR_E_ARG, "no scene uploaded");

@@ -476,7 +476,7 @@ int build_scene(const std::string& text, const char* obj_root, int64_t width, in
                     v = tuple3(l["vvec"], 0, "vvec");
             const Node& lv = l["level"];
             int64_t level = lv.kind == Node::Integer ? lv.i : 5;  // as_i64().unwrap_or(5)
-            if (level <= 0 || level > 64) panic("area light level out of range", RR_E_LIMIT);
+            if (level <= 0 || level > RR_MAX_AREA_LEVEL) panic("area light level out of range (1..RR_MAX_AREA_LEVEL)", RR_E_LIMIT);
             rr::Tup center = (corner + u * 0.5) + v * 0.5;  // light.rs:41-45
             const double vals[12] = {center.x, center.y, center.z, 0, 0, 0, corner.x, corner.y, corner.z, u.x, u.y, u.z};
             for (int k = 0; k < 3; ++k) rec[k] = vals[k];

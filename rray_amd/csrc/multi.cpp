@@ -21,7 +21,9 @@
 #include <string>
 #include <vector>
 
+#include "device_guard.hpp"
 #include "kernels.hpp"
+#include "partition.hpp"
 
 void rr_set_error(const char* msg);  // api.cpp
 
@@ -61,24 +63,15 @@ struct DevMem {
     }
 };
 
-int64_t rows_of(int64_t height, int32_t part, int32_t nparts, int32_t block) {
-    int64_t n = 0;
-    for (int64_t b0 = (int64_t)part * block; b0 < height; b0 += (int64_t)nparts * block)
-        n += std::min<int64_t>(block, height - b0);
-    return n;
-}
-
-// Gathered tiles -> frame order: output row y belongs to part p = (y / block) % nparts, where it is
-// local row j = (y / (block * nparts)) * block + y % block of p's padded tile.  One thread per double;
-// both sides are contiguous along a row.
+// Gathered tiles -> frame order (partition.hpp: the same index arithmetic as rr_unshuffle_host).  One
+// thread per double; both sides are contiguous along a row.
 __global__ void __launch_bounds__(256) unshuffle_kernel(const double* __restrict__ in, double* __restrict__ out,
                                                         int64_t row_len, int64_t height, int32_t nparts, int32_t block,
                                                         int64_t max_rows) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= row_len * height) return;
     const int64_t y = i / row_len, x = i - y * row_len;
-    const int64_t p = (y / block) % nparts, j = (y / ((int64_t)block * nparts)) * block + y % block;
-    out[i] = in[(p * max_rows + j) * row_len + x];
+    out[i] = in[rr::gathered_row_of(y, nparts, block, max_rows) * row_len + x];
 }
 
 hipError_t launch_unshuffle(const double* in, double* out, int64_t W, int64_t H, int32_t nparts, int32_t block,
@@ -99,12 +92,16 @@ struct rr_group {
     std::vector<ncclComm_t> comms;
     std::vector<hipStream_t> render_st, comm_st;
     std::vector<hipEvent_t> ev_rendered[2], ev_gathered[2];
+    bool virt = false;                    // rr_create_virtual: every part on one device, gather = local copies
     hipEvent_t ev_caller = nullptr;       // root: the caller's stream position at the gather call
-    std::vector<DevMem> tile[2];          // non-root local devices: their tile; root: unused
+    std::vector<DevMem> tile[2];          // non-root local parts: their tile; root: unused
     DevMem recv[2];                       // root: nranks x padded tile (slot 0 = its own tile, in place)
     DevMem frame;                         // root: assembled frame for the blocking rr_render
     int64_t k = 0;                        // frames issued (buffer = k % 2)
     bool root_here() const { return rank0 == 0; }
+    // the stream that gathers part l's tile (and releases its buffer): its own comm stream, or for a
+    // virtual group root's, where the copies into the receive buffer run
+    hipStream_t gather_stream(int l) const { return virt ? comm_st[0] : comm_st[l]; }
 };
 
 namespace rr {
@@ -138,6 +135,7 @@ static int group_setup(rr_group* g) {
 }
 
 int group_create_local(int n, const int* ids, rr_group** out) {
+    DeviceGuard device_guard;
     if (!out || n < 1 || !ids) return gfail(RR_E_ARG, "rr_create_multi: need n >= 1 device ids");
     *out = nullptr;
     int count = 0;
@@ -170,6 +168,7 @@ int group_create_local(int n, const int* ids, rr_group** out) {
 }
 
 int group_create_rank(int device, int nranks, int rank, const uint8_t* unique_id, rr_group** out) {
+    DeviceGuard device_guard;
     if (!out || nranks < 1 || rank < 0 || rank >= nranks || !unique_id)
         return gfail(RR_E_ARG, "rr_create_rank: need 0 <= rank < nranks and an RCCL unique id");
     *out = nullptr;
@@ -198,7 +197,30 @@ int group_create_rank(int device, int nranks, int rank, const uint8_t* unique_id
     return RR_OK;
 }
 
+int group_create_virtual(int device, int nparts, rr_group** out) {
+    DeviceGuard device_guard;
+    if (!out || nparts < 1) return gfail(RR_E_ARG, "rr_create_virtual: need nparts >= 1");
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return gfail(RR_E_HIP, "no HIP device available");
+    if (device < 0 || device >= count) return gfail(RR_E_ARG, "device index out of range");
+    rr_group* g = new rr_group();
+    g->nranks = nparts;
+    g->rank0 = 0;
+    g->virt = true;
+    g->devices.assign(nparts, device);  // one context (scene copy, workspace, streams) per part
+    int rc = group_setup(g);
+    if (rc != RR_OK) {
+        std::string msg = rr_last_error();
+        group_destroy(g);
+        return gfail(rc, msg);
+    }
+    *out = g;
+    return RR_OK;
+}
+
 void group_destroy(rr_group* g) {
+    DeviceGuard device_guard;
     if (!g) return;
     for (size_t l = 0; l < g->devices.size(); ++l) {
         (void)hipSetDevice(g->devices[l]);
@@ -228,6 +250,7 @@ void group_destroy(rr_group* g) {
 }
 
 int group_upload(rr_group* g, const rr_scene_desc* d) {
+    DeviceGuard device_guard;
     for (size_t l = 0; l < g->subs.size(); ++l) {  // the scene is replicated to every device (<= a few MB)
         GHIP(hipSetDevice(g->devices[l]));
         GHIP(hipStreamSynchronize(g->render_st[l]));
@@ -239,6 +262,7 @@ int group_upload(rr_group* g, const rr_scene_desc* d) {
 }
 
 int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts* o, void* d_frame, void* stream) {
+    DeviceGuard device_guard;
     if (!cam || !o) return gfail(RR_E_ARG, "null camera/options");
     if (o->nparts != 1 || o->part != 0)
         return gfail(RR_E_ARG, "a multi-device context splits the whole frame itself: pass part 0 of 1");
@@ -249,40 +273,63 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
     if (g->root_here() && !d_frame) return gfail(RR_E_ARG, "rank 0 needs a device frame buffer");
     const int32_t block = o->block_rows > 0 ? o->block_rows : 8;
     const int64_t W = cam->hsize / o->aa, H = cam->vsize / o->aa;
-    const int64_t max_rows = rows_of(H, 0, g->nranks, block);  // part 0 holds the most rows
-    const size_t count = (size_t)max_rows * (size_t)W * 3;       // doubles per (padded) tile
+    const int64_t max_rows = gather_tile_rows(H, g->nranks, block);
+    const size_t count = (size_t)max_rows * (size_t)W * 3;  // doubles per (padded) tile
     const int b = (int)(g->k & 1);
     const int n = (int)g->subs.size();
-    if (g->root_here()) {
-        GHIP(hipSetDevice(g->devices[0]));
-        GHIP(g->recv[b].ensure(count * g->nranks * sizeof(double)));
-        if (stream) GHIP(hipEventRecord(g->ev_caller, (hipStream_t)stream));
-    }
+    // every part's options and buffers are checked / allocated before any work is enqueued: a failure
+    // here returns before this rank joins the collective, never between its render and its gather
+    std::vector<rr_render_opts> opts(n, *o);
     for (int l = 0; l < n; ++l) {
-        GHIP(hipSetDevice(g->devices[l]));
-        const bool root = g->root_here() && l == 0;
-        if (!root) GHIP(g->tile[b][l].ensure(count * sizeof(double)));
-        void* t = root ? g->recv[b].p : g->tile[b][l].p;
-        // the gather that last read this buffer (two frames ago) must be done before it is overwritten
-        GHIP(hipStreamWaitEvent(g->render_st[l], g->ev_gathered[b][l], 0));
-        rr_render_opts so = *o;
+        rr_render_opts& so = opts[l];
         so.part = g->rank0 + l;
         so.nparts = g->nranks;
         so.block_rows = block;
         so.flags = RR_OUT_AVG | (o->flags & RR_NO_FRAME_TIMING);
-        int rc = rr_render_device(g->subs[l], cam, &so, nullptr, t, g->render_st[l]);
+        int rc = render_validate(g->subs[l], cam, &so);
+        if (rc != RR_OK) return rc;
+        GHIP(hipSetDevice(g->devices[l]));
+        if (g->root_here() && l == 0)
+            GHIP(g->recv[b].ensure(count * g->nranks * sizeof(double)));
+        else
+            GHIP(g->tile[b][l].ensure(count * sizeof(double)));
+    }
+    if (g->root_here() && stream) {
+        GHIP(hipSetDevice(g->devices[0]));
+        GHIP(hipEventRecord(g->ev_caller, (hipStream_t)stream));
+    }
+    for (int l = 0; l < n; ++l) {
+        GHIP(hipSetDevice(g->devices[l]));
+        const bool root = g->root_here() && l == 0;
+        void* t = root ? g->recv[b].p : g->tile[b][l].p;
+        // the gather that last read this buffer (two frames ago) must be done before it is overwritten
+        GHIP(hipStreamWaitEvent(g->render_st[l], g->ev_gathered[b][l], 0));
+        int rc = rr_render_device(g->subs[l], cam, &opts[l], nullptr, t, g->render_st[l]);
         if (rc != RR_OK) return rc;
         GHIP(hipEventRecord(g->ev_rendered[b][l], g->render_st[l]));
-        GHIP(hipStreamWaitEvent(g->comm_st[l], g->ev_rendered[b][l], 0));
+        GHIP(hipStreamWaitEvent(g->gather_stream(l), g->ev_rendered[b][l], 0));
     }
-    // one gather per frame: rank 0 receives rank r's tile at offset r * count (its own in place)
-    GNCCL(ncclGroupStart());
-    for (int l = 0; l < n; ++l) {
-        const bool root = g->root_here() && l == 0;
-        void* send = root ? g->recv[b].p : g->tile[b][l].p;
-        GNCCL(ncclGather(send, root ? g->recv[b].p : nullptr, count, ncclFloat64, 0, g->comms[l], g->comm_st[l]));
+    if (g->virt) {
+        // rank 0's receive buffer in ncclGather's layout: part l's tile at offset l * count (part 0 in place)
+        GHIP(hipSetDevice(g->devices[0]));
+        for (int l = 1; l < n; ++l)
+            GHIP(hipMemcpyAsync(static_cast<double*>(g->recv[b].p) + (size_t)l * count, g->tile[b][l].p,
+                                count * sizeof(double), hipMemcpyDeviceToDevice, g->comm_st[0]));
+    } else {
+        // one gather per frame: rank 0 receives rank r's tile at offset r * count (its own in place).  The
+        // RCCL group is always closed, also when a gather call fails.
+        ncclResult_t r = ncclGroupStart();
+        if (r == ncclSuccess) {
+            for (int l = 0; l < n && r == ncclSuccess; ++l) {
+                const bool root = g->root_here() && l == 0;
+                void* send = root ? g->recv[b].p : g->tile[b][l].p;
+                r = ncclGather(send, root ? g->recv[b].p : nullptr, count, ncclFloat64, 0, g->comms[l], g->comm_st[l]);
+            }
+            const ncclResult_t e = ncclGroupEnd();
+            if (r == ncclSuccess) r = e;
+        }
+        if (r != ncclSuccess) return gfail(RR_E_HIP, std::string("ncclGather: ") + ncclGetErrorString(r));
     }
-    GNCCL(ncclGroupEnd());
     for (int l = 0; l < n; ++l) {
         GHIP(hipSetDevice(g->devices[l]));
         if (g->root_here() && l == 0) {
@@ -290,7 +337,10 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
             GHIP(launch_unshuffle(static_cast<const double*>(g->recv[b].p), static_cast<double*>(d_frame), W, H,
                                   g->nranks, block, max_rows, g->comm_st[0]));
         }
-        GHIP(hipEventRecord(g->ev_gathered[b][l], g->comm_st[l]));
+    }
+    for (int l = 0; l < n; ++l) {  // after the unshuffle: a virtual group's buffers are all read on comm_st[0]
+        GHIP(hipSetDevice(g->devices[l]));
+        GHIP(hipEventRecord(g->ev_gathered[b][l], g->gather_stream(l)));
     }
     if (g->root_here() && stream) {
         GHIP(hipSetDevice(g->devices[0]));
@@ -302,6 +352,7 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
 
 int group_render(rr_group* g, const rr_camera* cam, const rr_render_opts* o, double* out_canvas, double* out_avg,
                  rr_stats* stats) {
+    DeviceGuard device_guard;
     if (!cam || !o) return gfail(RR_E_ARG, "null camera/options");
     if ((o->flags & RR_OUT_CANVAS) && out_canvas)
         return gfail(RR_E_ARG, "multi-device contexts produce the f64 AA-averaged image only (RR_OUT_AVG)");

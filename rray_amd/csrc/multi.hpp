@@ -15,6 +15,10 @@ namespace rr {
 // group takes ownership.  Global ranks rank0 .. rank0 + nlocal - 1 live in this process.
 int group_create_local(int n, const int* device_ids, rr_group** out);
 int group_create_rank(int device, int nranks, int rank, const uint8_t* unique_id, rr_group** out);
+// nparts virtual ranks on one device (rr_create_virtual): the same tiles, buffers, streams and
+// un-interleave as a real group, with the gather done by device-local copies into rank 0's receive
+// buffer in ncclGather's layout
+int group_create_virtual(int device, int nparts, rr_group** out);
 void group_destroy(rr_group* g);
 int group_upload(rr_group* g, const rr_scene_desc* d);
 int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts* o, void* d_frame, void* stream);
@@ -23,5 +27,7 @@ int group_render(rr_group* g, const rr_camera* cam, const rr_render_opts* o, dou
 int group_last_stats(rr_group* g, rr_stats* s);
 rr_ctx* group_local(rr_group* g, int l);  // local device context l (0 = the lowest global rank here)
 int group_info(const rr_group* g, int32_t* nranks, int32_t* rank0, int32_t* nlocal);
+// api.cpp: every argument check of rr_render_device, without enqueueing anything
+int render_validate(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o);
 
 }  // namespace rr

@@ -3,16 +3,19 @@
 Pixels are independent (camera.rs:110-118 renders them in any order), so rank r renders the output
 rows {y : (y // block) % N == r} (interleaved blocks balance sky/floor cost) and one collective
 (torch.distributed.gather; backend "nccl" is RCCL over xGMI on ROCm, "gloo" on CPU tests) brings
-the tiles to rank 0, which scatters the rows back into frame order.
+the tiles to rank 0, which scatters the rows back into frame order.  The gather buffer layout and the
+un-interleave are the library's (partition.hpp, rr_unshuffle_host): the same arithmetic as the C ABI's
+own multi-GPU path (multi.cpp), so CPU rehearsals of this module exercise it.
 
 FramePipeline double-buffers the tiles so that rendering frame k+1 overlaps the gather of frame k
 (the gather runs on the process group's own stream; the renderer waits only for the gather that
 last read the buffer it is about to overwrite).
 """
+import numpy as np
 import torch
 import torch.distributed as dist
 
-from .render import part_rows
+from .render import part_rows, unshuffle
 
 
 def tile_rows(height, rank, world, block=8):
@@ -20,23 +23,39 @@ def tile_rows(height, rank, world, block=8):
 
 
 def max_tile_rows(height, world, block=8):
-    return max(len(part_rows(height, p, world, block)) for p in range(world))
+    """Padded rows per tile in the gather buffer (part 0 holds the most rows; partition.hpp)."""
+    return len(part_rows(height, 0, world, block))
+
+
+def gather_sources(height, world, block=8):
+    """For every output row y, its row in the gathered buffer (world tiles of max_tile_rows rows back
+    to back, ncclGather's layout), computed by the library's own un-interleave (rr_unshuffle_host, the
+    index arithmetic of multi.cpp's device kernel) applied to a buffer whose rows hold their indices."""
+    rows = max_tile_rows(height, world, block)
+    idx = np.repeat(np.arange(world * rows, dtype=np.float64), 3).reshape(world * rows, 1, 3)
+    return unshuffle(idx, height, world, block)[:, 0, 0].astype(np.int64)
 
 
 def gather_frame(tile, height, block=8, dst=0, group=None, out=None):
-    """tile: (max_tile_rows, W, C) with this rank's rows first.  Returns the (height, W, C) frame on
-    `dst` (written into `out` when given), None on the other ranks."""
+    """tile: (max_tile_rows, W, C) with this rank's rows first (padding after).  One gather into a
+    contiguous (world * max_tile_rows, W, C) buffer on `dst` — the layout multi.cpp's ncclGather
+    produces — then the library's un-interleave.  Returns the (height, W, C) frame on `dst` (written
+    into `out` when given), None on the other ranks."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    gl = [torch.empty_like(tile) for _ in range(world)] if rank == dst else None
-    dist.gather(tile, gather_list=gl, dst=dst, group=group)
+    big = torch.empty((world,) + tuple(tile.shape), dtype=tile.dtype, device=tile.device) if rank == dst else None
+    dist.gather(tile, gather_list=list(big.unbind(0)) if big is not None else None, dst=dst, group=group)
     if rank != dst:
         return None
-    frame = out if out is not None else torch.empty((height,) + tuple(tile.shape[1:]), dtype=tile.dtype,
-                                                      device=tile.device)
-    for p in range(world):
-        rows = torch.as_tensor(part_rows(height, p, world, block), device=tile.device)
-        frame.index_copy_(0, rows, gl[p][: len(rows)])
+    flat = big.view(world * tile.shape[0], *tile.shape[1:])
+    if tile.device.type == "cpu" and tile.dtype == torch.float64 and tile.shape[-1] == 3:
+        frame = torch.from_numpy(unshuffle(flat.numpy(), height, world, block))  # rr_unshuffle_host
+    else:
+        src = torch.as_tensor(gather_sources(height, world, block), device=tile.device)
+        frame = torch.index_select(flat, 0, src)
+    if out is not None:
+        out.copy_(frame)
+        return out
     return frame
 
 
@@ -59,11 +78,7 @@ class FramePipeline:
         if self.rank == dst:
             self.big = torch.empty((self.world,) + shape, dtype=dtype, device=device)
             self.gl = list(self.big.unbind(0))
-            src = [0] * height
-            for p in range(self.world):
-                for j, y in enumerate(part_rows(height, p, self.world, block)):
-                    src[y] = p * self.rows + j
-            self.src = torch.as_tensor(src, dtype=torch.long, device=device)
+            self.src = torch.as_tensor(gather_sources(height, self.world, block), dtype=torch.long, device=device)
             self.frame = torch.empty((height, width, channels), dtype=dtype, device=device)
 
     def acquire(self):

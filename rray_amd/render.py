@@ -226,6 +226,16 @@ def part_rows(height, part, nparts, block_rows=8):
     return out[:n]
 
 
+def unshuffle(gathered, height, nparts, block_rows=8):
+    """rr_unshuffle_host: the root's un-interleave on the host.  gathered: (nparts * tile_rows, W, 3) f64 in
+    ncclGather's layout (tile_rows = len(part_rows(height, 0, nparts, block_rows)))."""
+    g = np.ascontiguousarray(gathered, np.float64)
+    W = g.shape[1]
+    frame = np.zeros((height, W, 3), np.float64)
+    check(lib().rr_unshuffle_host(_dp(g), _dp(frame), W, height, nparts, block_rows))
+    return frame
+
+
 def device_count():
     n = C.c_int(0)
     lib().rr_device_count(C.byref(n))
@@ -264,6 +274,14 @@ class Renderer:
         uid = (C.c_uint8 * _lib.RCCL_ID_BYTES).from_buffer_copy(unique_id)
         h = C.c_void_p()
         check(lib().rr_create_rank(device, nranks, rank, uid, C.byref(h)))
+        return cls(device, _handle=h)
+
+    @classmethod
+    def virtual(cls, device, nparts):
+        """rr_create_virtual: nparts virtual ranks on one device (the multi-GPU frame assembly with the
+        RCCL transfer replaced by device-local copies)."""
+        h = C.c_void_p()
+        check(lib().rr_create_virtual(device, nparts, C.byref(h)))
         return cls(device, _handle=h)
 
     def info(self):

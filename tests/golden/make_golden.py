@@ -16,7 +16,9 @@ sys.path.insert(0, ROOT)
 from oracle.scene_yaml import build_from_yaml  # noqa: E402
 
 CASES = [("c1_readme.yaml", 40, 30, 2, 0), ("c2_s1024.yaml", 48, 27, 1, 0), ("c3_s1024_reflect.yaml", 32, 18, 2, 0),
-         ("c4_teapot.yaml", 32, 18, 1, 0), ("c5_area_light.yaml", 32, 16, 2, 3)]
+         ("c4_teapot.yaml", 32, 18, 1, 0), ("c5_area_light.yaml", 32, 16, 2, 3),
+         # each config at its own AA level (BASELINE configs: C3 aa=3, C4 aa=2)
+         ("c3_s1024_reflect.yaml", 32, 18, 3, 0), ("c4_teapot.yaml", 32, 18, 2, 0)]
 
 
 def main():

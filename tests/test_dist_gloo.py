@@ -1,7 +1,8 @@
-"""world_size-2 gloo test of the multi-GPU path's host logic on CPU: the row partition + gather +
-un-interleave (rray_amd/dist.py) reassemble a frame bit-identical to the single-process render.
-The tiles are rendered by the oracle here (test stand-in for the GPU; the GPU test
-test_multi_part_tiles_are_bit_identical covers the kernels)."""
+"""world_size-2/3 gloo tests of the multi-GPU path's host logic on CPU: the row partition, the padded
+tiles gathered back to back (multi.cpp's ncclGather layout) and the library's un-interleave
+(rr_unshuffle_host, the index arithmetic of multi.cpp's device kernel) reassemble a frame bit-identical
+to the single-process render, in f64 like the product's tiles.  The tiles are rendered by the oracle here
+(test stand-in for the GPU; the GPU tests test_virtual_group_* run the same assembly on the device)."""
 import os
 import socket
 
@@ -60,14 +61,14 @@ def _pipe_worker(rank, world, port, W, H, block, q):
     o, cam = build_from_yaml(text, W, H, 1)
     canvas, _ = o.render(cam, max_depth=5, threads=2, band=block, band_stride=world, band_phase=rank)
     rows = rdist.tile_rows(H, rank, world, block)
-    pipe = rdist.FramePipeline(H, W, 3, torch.float32, torch.device("cpu"), block=block)
+    pipe = rdist.FramePipeline(H, W, 3, torch.float64, torch.device("cpu"), block=block)
     frames = []
     for k in range(3):  # three frames: both buffers reused once
         i, tile, prev = pipe.acquire()
         if prev is not None:
             prev.wait()
         tile.zero_()
-        tile[: len(rows)] = torch.from_numpy(canvas[rows] * (k + 1)).float()
+        tile[: len(rows)] = torch.from_numpy(canvas[rows] * (k + 1))
         pipe.submit(i)
         if rank == 0:
             frames.append(pipe.frame.clone().numpy())
@@ -98,10 +99,10 @@ def test_two_rank_pipelined_gather(oracle_mod):
     o, cam = build_from_yaml(text, W, H, 1)
     full, _ = o.render(cam, max_depth=5, threads=2)
     for k, fr in enumerate(frames):
-        assert np.array_equal(fr, (full * (k + 1)).astype(np.float32))
+        assert np.array_equal(fr, full * (k + 1))
 
 
-@pytest.mark.parametrize("world,H", [(2, 36), (2, 33)])
+@pytest.mark.parametrize("world,H", [(2, 36), (2, 33), (3, 30)])
 def test_two_rank_gather_matches_single_render(oracle_mod, world, H):
     from oracle.scene_yaml import build_from_yaml
 
@@ -122,3 +123,21 @@ def test_two_rank_gather_matches_single_render(oracle_mod, world, H):
     o, cam = build_from_yaml(text, W, H, 1)
     full, _ = o.render(cam, max_depth=5, threads=2)
     assert np.array_equal(frame, full)
+
+
+def test_host_unshuffle_matches_partition():
+    """rr_unshuffle_host (the device kernel's index arithmetic on the host) inverts the row partition for
+    part counts that do not divide the height, including parts with no rows at all (8 parts of 5 blocks)."""
+    import rray_amd as R
+
+    rng = np.random.default_rng(3)
+    for H, world, block in ((40, 2, 8), (40, 3, 8), (40, 8, 8), (33, 2, 4), (7, 4, 2), (1, 3, 8)):
+        W = 5
+        frame = rng.standard_normal((H, W, 3))
+        rows = len(R.part_rows(H, 0, world, block))
+        gathered = np.full((world * rows, W, 3), np.nan)
+        for p in range(world):
+            pr = R.part_rows(H, p, world, block)
+            assert len(pr) <= rows
+            gathered[p * rows: p * rows + len(pr)] = frame[pr]
+        assert np.array_equal(R.unshuffle(gathered, H, world, block), frame), (H, world, block)

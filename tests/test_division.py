@@ -52,12 +52,16 @@ def test_div_y_signed_zeros_and_unit_vectors():
 
 
 def test_area_cell_offsets():
-    """(col + u) / level for every level up to 64, u with 32 random bits (jitter_value)."""
+    """(col + u) / level for every level up to RR_MAX_AREA_LEVEL (1024, rray.h), u with 32 random bits
+    (jitter_value), including the extreme cells (col 0 with u = 0, col level-1 with u just below 1).
+    Markstein's theorem covers every level (y = RN(1/level), q0 faithful, the residual exact in one fma);
+    the samples check the implementation of it."""
     rnd = random.Random(11)
-    for level in range(1, 65):
+    for level in range(1, 1025):
         y = 1.0 / level
-        for _ in range(300):
-            col = rnd.randrange(level)
-            u = rnd.getrandbits(32) * (1.0 / 4294967296.0)
+        cases = [(0, 0.0), (level - 1, (2**32 - 1) / 4294967296.0)]
+        cases += [(rnd.randrange(level), rnd.getrandbits(32) * (1.0 / 4294967296.0))
+                  for _ in range(40 if level <= 64 else 8)]
+        for col, u in cases:
             n = col + u
-            assert same(div_y(n, float(level), y), n / level)
+            assert same(div_y(n, float(level), y), n / level), (level, col, u)

@@ -1,10 +1,12 @@
 """GPU tests of the multi-device contexts (rr_create_multi / rr_create_rank: row tiles + one RCCL
 gather) and of the drop-in CLI end to end (main.rs:49-77 -> PNG on disk).
 
-The GPU box has one MI355X, so the groups here have one device / one rank: they exercise the whole
+The GPU box has one MI355X, so the RCCL groups here have one device / one rank: they exercise the whole
 path through the C ABI (tile render into the gather buffer, ncclGather on a 1-rank communicator, the
-un-interleave kernel, double-buffered pipelining); the partition arithmetic for N > 1 is covered by
-test_multi_part_tiles_are_bit_identical (GPU) and tests/test_dist_gloo.py (CPU).
+un-interleave kernel, double-buffered pipelining).  The N > 1 frame assembly runs through virtual groups
+(rr_create_virtual): N parts on the one device, each with its own context and streams, padded tiles
+copied into rank 0's receive buffer in ncclGather's layout, the un-interleave kernel with nparts = N —
+everything of the N > 1 path except the RCCL transfer itself.
 """
 import ctypes
 import os
@@ -59,6 +61,65 @@ def test_group_context_matches_single_device(R, single, kind):
             assert got["stats"][k] == ref["stats"][k], k
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("nparts", [2, 3, 8])
+def test_virtual_group_assembles_the_frame(R, single, nparts):
+    """N virtual ranks (row tiles, padded gather layout, un-interleave kernel with nparts = N) reassemble
+    the 1-part image bit for bit.  40 output rows = 5 blocks of 8: not a multiple of 8N for any N here,
+    so tiles are padded, and at N = 8 three parts own no rows at all.  C3's scene (reflection chains,
+    depth 5) at its own AA."""
+    W, H, aa = 48, 40, 3
+    scene = _scene(R, "c3_s1024_reflect.yaml", W, H, aa)
+    single.upload(scene)
+    ref = single.render(scene.camera, aa=aa)
+    g = R.Renderer.virtual(0, nparts)
+    try:
+        assert g.info() == (nparts, 0, nparts)
+        g.upload(scene)
+        got = g.render(scene.camera, aa=aa)
+        assert np.array_equal(got["avg"], ref["avg"])
+        for k in ("rays", "shadow_rays", "shade_events", "samples"):
+            assert got["stats"][k] == ref["stats"][k], k
+    finally:
+        g.close()
+
+
+def test_virtual_group_pipelined_frames(R, single):
+    """rr_render_gather_device on 3 virtual ranks: three frames from two cameras enqueued back to back
+    (double-buffered tiles and receive buffers) land in their own buffers unchanged."""
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    W, H, aa = 64, 44, 2
+    scene = _scene(R, "c3_s1024_reflect.yaml", W, H, aa)
+    cam_a = scene.camera
+    cam_b = R.camera(cam_a.hsize, cam_a.vsize, cam_a.field_of_view * 0.75, list(cam_a.transform))
+    single.upload(scene)
+    refs = [single.render(c, aa=aa)["avg"] for c in (cam_a, cam_b)]
+    g = R.Renderer.virtual(0, 3)
+    bufs = []
+    try:
+        g.upload(scene)
+        nbytes = refs[0].size * 8
+        for _ in range(3):
+            d = ctypes.c_void_p()
+            assert hip.hipMalloc(ctypes.byref(d), ctypes.c_size_t(nbytes)) == 0
+            bufs.append(d)
+        opts = R._lib.RenderOpts(aa, 5, 0, 0, 0, 1, 8, R._lib.RR_OUT_AVG | R._lib.RR_NO_FRAME_TIMING)
+        for cam, d in zip((cam_a, cam_b, cam_a), bufs):
+            g.render_gather_device(cam, opts, d.value, None)
+        assert hip.hipDeviceSynchronize() == 0
+        outs = []
+        for d in bufs:
+            out = np.empty_like(refs[0])
+            assert hip.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), d, ctypes.c_size_t(nbytes), 2) == 0
+            outs.append(out)
+    finally:
+        for d in bufs:
+            hip.hipFree(d)
+        g.close()
+    assert np.array_equal(outs[0], refs[0])
+    assert np.array_equal(outs[1], refs[1])
+    assert np.array_equal(outs[2], refs[0])
 
 
 def test_group_rejects_part_and_canvas(R):

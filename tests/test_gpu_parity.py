@@ -58,7 +58,9 @@ CASES = [  # (scene file, W, H, aa)
     ("c1_readme.yaml", 32, 24, 3),
     ("c2_s1024.yaml", 64, 36, 1),
     ("c3_s1024_reflect.yaml", 48, 27, 2),
+    ("c3_s1024_reflect.yaml", 32, 18, 3),  # C3's own AA
     ("c4_teapot.yaml", 48, 27, 1),
+    ("c4_teapot.yaml", 48, 27, 2),  # C4's own AA
     ("c5_area_light.yaml", 40, 20, 2),
 ]
 
@@ -79,10 +81,12 @@ def test_render_matches_oracle(renderer, name, W, H, aa):
 
 
 def test_render_matches_committed_golden(renderer, R):
-    """Committed oracle outputs (tests/golden/make_golden.py) — no live oracle needed."""
+    """Committed oracle outputs (tests/golden/make_golden.py) — no live oracle needed.  Every config
+    scene, C3 and C4 also at their own AA levels (3 and 2)."""
     import json
 
     meta = json.load(open(os.path.join(GOLDEN, "golden_renders.json")))
+    assert {(g["scene"], g["aa"]) for g in meta} >= {("c3_s1024_reflect.yaml", 3), ("c4_teapot.yaml", 2)}
     for g in meta:
         scene = R.YamlScene(open(os.path.join(SCENES, g["scene"])).read(), g["W"], g["H"], g["aa"], obj_root=SCENES)
         renderer.upload(scene)
@@ -144,6 +148,31 @@ def test_reference_png_through_gpu(renderer, R, name, png, aa):
     diff = int((q != ref).any(axis=2).sum())
     print(f"{png}: {diff} of {ref.shape[0] * ref.shape[1]} pixels differ")
     assert diff == 0
+
+
+def test_c1_readme_test1_png_through_gpu(renderer, R):
+    """C1 pinned to the reference's own image: examples/test1.png is the README scene (README.md:106-113,
+    `rray -W 800 -H 400`, aa=1).  The glass sphere exercises reflect + refract + Schlick + n1/n2."""
+    PIL = pytest.importorskip("PIL.Image")
+    text = open(os.path.join(SCENES, "c1_readme.yaml")).read()
+    scene = R.YamlScene(text, 800, 400, 1, obj_root=SCENES)
+    renderer.upload(scene)
+    avg = renderer.render(scene.camera, aa=1, max_depth=5)["avg"]
+    q = R.quantize(avg)[..., :3]
+    ref = np.asarray(PIL.open(os.path.join(GOLDEN, "png", "test1.png")).convert("RGB"))
+    diff = int((q != ref).any(axis=2).sum())
+    print(f"test1.png: {diff} of {ref.shape[0] * ref.shape[1]} pixels differ")
+    assert diff == 0
+
+
+def test_c1_config_full_frame(renderer):
+    """BASELINE configs[0]: the README scene at 800x600 aa=1, whole frame against the oracle."""
+    scene, (o, cam) = _yaml_pair("c1_readme.yaml", 800, 600, 1)
+    renderer.upload(scene)
+    got = renderer.render(scene.camera, aa=1, max_depth=5)
+    canvas, st = o.render(cam, max_depth=5, threads=0)
+    _compare(got["avg"], o.aa_average(canvas, 1), "c1 800x600 aa1")
+    assert got["stats"]["shade_events"] == st["shade_events"]
 
 
 def test_example1_png_through_gpu(renderer, R):

@@ -45,6 +45,24 @@ def test_oracle_reproduces_reference_png(oracle_mod, scene, png, aa):
     assert diff == 0, f"{diff} pixels differ from the reference's {png}"
 
 
+def test_oracle_reproduces_readme_test1(oracle_mod):
+    """C1's own golden: examples/test1.png is the README scene (README.md:56-113, committed as
+    scenes/c1_readme.yaml) rendered by `rray -W 800 -H 400` at the CLI's default aa=1 (main.rs:49-71).
+    The only reference-held image of the glass sphere (reflective 0.9, transparency 0.1): reflect,
+    refract, Schlick and the n1/n2 container walk together."""
+    pytest.importorskip("PIL")
+    from oracle.scene_yaml import build_from_yaml
+
+    text = open(os.path.join(ROOT, "scenes", "c1_readme.yaml")).read()
+    o, cam = build_from_yaml(text, 800, 400, 1, obj_root=os.path.join(ROOT, "scenes"))
+    canvas, st = o.render(cam, max_depth=5, threads=min(8, os.cpu_count() or 1))
+    assert st["shade_events"] > 0
+    q = o.quantize(o.aa_average(canvas, 1))[..., :3]
+    ref = _png_rgb(os.path.join(GOLDEN, "png", "test1.png"))
+    diff = int((q != ref).any(axis=2).sum())
+    assert diff == 0, f"{diff} pixels differ from the reference's test1.png"
+
+
 def test_oracle_reproduces_example1(oracle_mod):
     """/root/reference/example1.png (800x400, aa=3) from example1.yaml with its examples/ files."""
     pytest.importorskip("PIL")
@@ -59,3 +77,20 @@ def test_oracle_reproduces_example1(oracle_mod):
     ref = _png_rgb(os.path.join(root, "example1.png"))
     diff = int((q != ref).any(axis=2).sum())
     assert diff == 0, f"{diff} pixels differ from the reference's example1.png"
+
+
+def test_committed_golden_renders_match_live_oracle(oracle_mod):
+    """tests/golden/oracle_*.npy (the GPU suite's committed vectors, make_golden.py) are what the pinned
+    oracle renders today, including each BASELINE config at its own AA (C3 aa=3, C4 aa=2)."""
+    import json
+
+    from oracle.scene_yaml import build_from_yaml
+
+    meta = json.load(open(os.path.join(GOLDEN, "golden_renders.json")))
+    assert {(g["scene"], g["aa"]) for g in meta} >= {("c3_s1024_reflect.yaml", 3), ("c4_teapot.yaml", 2)}
+    for g in meta:
+        text = open(os.path.join(ROOT, "scenes", g["scene"])).read()
+        o, cam = build_from_yaml(text, g["W"], g["H"], g["aa"], obj_root=os.path.join(ROOT, "scenes"))
+        canvas, st = o.render(cam, max_depth=5, seed=g["seed"], threads=min(8, os.cpu_count() or 1))
+        assert np.array_equal(o.aa_average(canvas, g["aa"]), np.load(os.path.join(GOLDEN, g["file"]))), g["file"]
+        assert st["rays"] == g["stats"]["rays"] and st["shade_events"] == g["stats"]["shade_events"], g["file"]

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for spec in "$@"; do
   IFS='|' read -r label lib envs <<< "$spec"
-  ( [ -n "$lib" ] && export RRAY_LIB=$PWD/$lib
+  ( [ -n "$lib" ] && export RRAY_EXPERIMENT=1 RRAY_LIB=$PWD/$lib
     for kv in ${envs//;/ }; do export "$kv"; done
     timeout -k 10 200 python bench.py ${BENCH_ARGS:---steps 20 --warmup 3} > gpurun_out/ab_$label.log 2>&1 ) || { echo "$label failed"; tail -5 gpurun_out/ab_$label.log; exit 1; }
   tail -1 gpurun_out/ab_$label.log | python -c "

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 for v in ${VARIANTS:-default}; do
   case $v in
     default) env="RRAY_X=0";;
-    *) env="RRAY_LIB=$PWD/abtest/$v/librray_amd.so";;
+    *) env="RRAY_EXPERIMENT=1 RRAY_LIB=$PWD/abtest/$v/librray_amd.so";;
   esac
   env $env timeout -k 10 200 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/bv_$v.log 2>&1 || exit 1
   python3 -c "

@@ -9,7 +9,7 @@ for v in ${VARIANTS:-default}; do
   case $v in
     default) env="RRAY_X=0";;
     unfused) env="RRAY_UNFUSED=1";;
-    *) env="RRAY_LIB=$PWD/abtest/$v/librray_amd.so";;
+    *) env="RRAY_EXPERIMENT=1 RRAY_LIB=$PWD/abtest/$v/librray_amd.so";;
   esac
   for r in 1 2; do
     echo "== $v run $r"

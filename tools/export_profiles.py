@@ -41,7 +41,11 @@ def export(tag, wl):
                   "SQ_INSTS_SALU | FETCH_SIZE | WRITE_SIZE), tools/profile_all.sh",
     }
     json.dump(summary, open(os.path.join(out_dir, f"{wl}_summary.json"), "w"), indent=1)
+    dig = os.path.join(src, "src_digest")
+    summary["src_digest"] = open(dig).read().strip() if os.path.exists(dig) else None
+    json.dump(summary, open(os.path.join(out_dir, f"{wl}_summary.json"), "w"), indent=1)
     json.dump({"trace_shade": {"hbm_bytes_per_launch": summary["hbm_bytes_per_launch"], "valu_busy_frac": summary["valu_busy"],
+                               "src_digest": summary["src_digest"],
                                "rocprof_avg_ns": summary["mean_launch_us"] * 1e3,
                                "profile": f"profiles/{tag}/{wl}_summary.json"}},
               open(os.path.join(ROOT, "profiles", f"pmc_{wl}.json"), "w"), indent=1)

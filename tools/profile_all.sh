@@ -11,4 +11,5 @@ for wl in ${WLS:-c2_s1024 c3_s1024_reflect c4_teapot c5_area_light}; do
     bash tools/profile_session.sh > "gpurun_out/prof_$wl.log" 2>&1 || { echo "$wl profile failed"; tail -5 "gpurun_out/prof_$wl.log"; exit 1; }
   echo "== $wl"
   python tools/profile_levels.py "gpurun_out/prof_$wl" "gpurun_out/prof_$wl/levels.json" || exit 1
+  python -c "from rray_amd.build import source_digest; print(source_digest())" > "gpurun_out/prof_$wl/src_digest"
 done
