@@ -97,6 +97,7 @@ def _load():
         L.orc_jitter.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
         L.orc_jitter.restype = C.c_double
         L.orc_set_context.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_uint64]
+        L.orc_set_pow_mode.argtypes = [C.c_void_p, C.c_int]
         L.orc_get_stats.argtypes = [C.c_void_p, C.POINTER(OrcStats)]
         L.orc_set_shape_params.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_int]
         L.orc_set_csg_op.argtypes = [C.c_void_p, C.c_int, C.c_int]
@@ -340,6 +341,11 @@ class Oracle:
         o = _out(16)
         self.L.orc_get_inverse(self.w, oid, o)
         return list(o)
+
+    def set_pow_mode(self, mode):
+        """DIAGNOSTIC: 1 = correctly rounded x^n for integer shininess (libm pow is not always correctly
+        rounded); 0 = std::pow as the reference (the default, and the parity reference)."""
+        self.L.orc_set_pow_mode(self.w, int(mode))
 
     def set_context(self, seed=0, jitter_mode=0, sample=0):
         self.L.orc_set_context(self.w, seed, jitter_mode, sample)

@@ -320,6 +320,11 @@ struct orc_world {
     std::vector<Pattern> patterns;
     Ctx ctx;  // context used by the single-ray query API
     bool dirty = true;  // group AABB caches need (re)building (group.rs:54-67 invalidation)
+    // DIAGNOSTIC ONLY (never the reference's semantics): 1 = the specular power of an integer shininess
+    // n in [0, 512] correctly rounded (x^n in binary128, then rounded once) instead of libm pow.  libm's
+    // pow (what the reference's f64::powf calls) is within 0.52 ulp, not always correctly rounded; the
+    // fuzz test uses this mode to tell a last-ulp pow difference from a walk error.
+    int pow_mode = 0;
 };
 
 namespace {
@@ -1244,7 +1249,17 @@ Color lighting(const orc_world* w, int obj, const Light& light, const Tuple& poi
         if (rde <= 0.0) {
             specular = BLACK;
         } else {
-            double factor = std::pow(rde, m.shininess);
+            double factor;
+            if (w->pow_mode == 1 && m.shininess >= 0.0 && m.shininess <= 512.0 && m.shininess == std::floor(m.shininess)) {
+                __float128 x = rde, r = 1;  // exact squaring chain: 113-bit products, one final rounding
+                for (unsigned n = (unsigned)m.shininess; n; n >>= 1) {
+                    if (n & 1u) r *= x;
+                    x *= x;
+                }
+                factor = (double)r;
+            } else {
+                factor = std::pow(rde, m.shininess);
+            }
             specular = cmul(cmul(light.intensity, m.specular), factor);
         }
     }
@@ -1554,6 +1569,8 @@ void orc_pattern_info(orc_world* w, int id, int32_t ints[3], double dbl[2], int6
     *octaves = p.octaves;
 }
 void orc_get_inverse(orc_world* w, int id, double out[16]) { to16(w->objects[id].inv, out); }
+
+void orc_set_pow_mode(orc_world* w, int mode) { w->pow_mode = mode; }
 
 void orc_set_context(orc_world* w, uint64_t seed, int jitter_mode, uint64_t sample) {
     w->ctx.seed = seed;

@@ -147,6 +147,7 @@ void orc_quantize(const double* avg, int64_t n_pixels, uint8_t* rgba);
 /* counter-based area-light jitter shared with the HIP kernel */
 double orc_jitter(uint64_t seed, uint64_t sample, uint32_t path, uint32_t light, uint32_t s, uint32_t which);
 void   orc_set_context(orc_world* w, uint64_t seed, int jitter_mode, uint64_t sample);
+void   orc_set_pow_mode(orc_world* w, int mode);  /* diagnostic: 1 = correctly rounded integer powers */
 void   orc_get_stats(orc_world* w, orc_stats* out);
 
 #ifdef __cplusplus

@@ -11,7 +11,7 @@ import pytest
 
 import scene_fuzz as F  # noqa: E402
 
-SEEDS = range(48)
+SEEDS = range(96)
 
 
 @pytest.mark.parametrize("seed", SEEDS)
