@@ -199,8 +199,16 @@ LevelPlan plan_levels(int64_t nb, int k, int max_depth, bool ext, bool fused = f
     return p;
 }
 
+// The averaged image can be written by the level-0 waves themselves (deliver_wave_avg) when every
+// pixel's samples lie in one wave's 8x8 tile (aa in {2, 4, 8}, full tiles: the tile_fast layout) and no
+// sample spawns a secondary ray (fused levels with no reflective / transparent material, or depth 0).
+bool wave_avg_ok(const rr_ctx* c, int32_t aa, int64_t hs, int64_t local_rows, int max_depth) {
+    return (aa == 2 || aa == 4 || aa == 8) && hs % 8 == 0 && local_rows % 8 == 0 && local_rows > 0 &&
+           rr::fused_levels(c->S) && (c->host.max_children == 0 || max_depth == 0);
+}
+
 int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max_depth, double* out, hipStream_t st,
-               void* avg = nullptr, int32_t avg_f32 = 0) {
+               void* avg = nullptr, int32_t avg_f32 = 0, int32_t aa_wave = 0) {
     const int k = c->host.max_children;
     const bool ext = c->host.has_transparent != 0;
     const bool fused = rr::fused_levels(c->S);
@@ -271,6 +279,8 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             A.out = out;
             A.avg = avg;
             A.avg_f32 = avg_f32;
+            A.aa_wave = (d == 0 && A.tile_fast) ? aa_wave : 0;
+            if (aa_wave && !A.aa_wave) return fail(RR_E_ARG, "internal: in-wave AA average without full tiles");
             // null when no material is reflective or transparent (or at the last level)
             A.next = children_possible ? (d % 2 ? c->ev_b : c->ev_a).as<rr::Event>() : nullptr;
             A.pending = children_possible ? c->pend[d].as<int32_t>() : nullptr;
@@ -568,6 +578,7 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     S.has_area = 0;
     for (const rr::DevLight& l : c->host.lights) S.has_area |= l.kind == RR_LIGHT_AREA ? 1 : 0;
     S.complex_patterns = c->host.complex_patterns;
+    S.tri_inline = c->host.tri_inline;
     S.has_groups = c->host.groups.empty() ? 0 : 1;
     S.general = (c->host.has_csg || c->host.has_quad) ? 1 : 0;
     const size_t lds_bytes = (size_t)S.n_nodes * sizeof(rr::DevCull) + (size_t)S.n_chunks * sizeof(rr::DevChunk);
@@ -611,7 +622,9 @@ int rr_scene_inspect(const rr_scene_desc* d, double* inverses, double* group_aab
         if (node_of_object) node_of_object[i] = node;
         if (inverses) {
             double* o = inverses + 16 * (size_t)i;
-            if (node >= 0) {
+            if (node >= 0 && (hs.nodes[node].flags & rr::NF_TRI_INLINE)) {  // identity (slots hold p1/e1/e2)
+                for (int k = 0; k < 12; ++k) o[k] = (k % 5 == 0) ? 1.0 : 0.0;
+            } else if (node >= 0) {
                 for (int k = 0; k < 12; ++k) o[k] = hs.nodes[node].inv[k];
             } else {
                 for (int k = 0; k < 12; ++k) o[k] = 0.0;
@@ -705,8 +718,10 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     // a render on a different stream than the previous one first waits for that one.
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
     HIPCHK(claim_stream(c, st));
-    // aa == 1: the average is written by the kernels directly; the canvas only when asked for
-    const bool direct_avg = o->aa == 1 && d_avg;
+    // aa == 1, or aa in {2, 4, 8} without secondary rays (wave_avg_ok): the average is written by the
+    // kernels directly; the canvas only when asked for
+    const bool wave_avg = d_avg && wave_avg_ok(c, o->aa, cam->hsize, local_rows, o->max_depth);
+    const bool direct_avg = d_avg && (o->aa == 1 || wave_avg);
     double* canvas = static_cast<double*>(d_canvas);
     if (!canvas && !direct_avg) {
         HIPCHK(c->canvas.ensure(std::max<int64_t>(total, 1) * 3 * sizeof(double)));
@@ -729,7 +744,7 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     A.jitter_mode = o->jitter_mode;
     const int32_t f32 = (o->flags & RR_OUT_AVG_F32) ? 1 : 0;
     c->zero_next = true;
-    rc = run_levels(c, A, total, o->max_depth, canvas, st, direct_avg ? d_avg : nullptr, f32);
+    rc = run_levels(c, A, total, o->max_depth, canvas, st, direct_avg ? d_avg : nullptr, f32, wave_avg ? o->aa : 0);
     c->zero_next = false;
     if (rc != RR_OK) return rc;
     c->stats_src = frame_counters(c, c->epoch);

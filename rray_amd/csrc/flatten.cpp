@@ -685,6 +685,24 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
     }
     reorder_spatial(out);
     build_chunks(out);
+    // identity-transform triangles carry their Möller-Trumbore data in the (unused) inverse slots, after
+    // every use of the stored inverses above (culls); the kernels and rr_scene_inspect know NF_TRI_INLINE
+    int n_tri = 0, n_inline = 0;
+    for (DevNode& nd : out.nodes) {
+        if (nd.kind != RR_TRIANGLE && nd.kind != RR_SMOOTH_TRIANGLE) continue;
+        ++n_tri;
+        if (!(nd.flags & NF_IDENT)) continue;
+        const DevTri& t = out.tris[nd.aux];
+        for (int c = 0; c < 3; ++c) {
+            nd.inv[c] = t.p1[c];
+            nd.inv[3 + c] = t.e1[c];
+            nd.inv[6 + c] = t.e2[c];
+        }
+        nd.inv[9] = nd.inv[10] = nd.inv[11] = 0.0;
+        nd.flags |= NF_TRI_INLINE;
+        ++n_inline;
+    }
+    out.tri_inline = n_tri > 0 && n_inline == n_tri ? 1 : 0;
     return RR_OK;
 }
 

@@ -24,6 +24,7 @@ struct HostScene {
     int32_t has_transparent = 0;
     int32_t has_secondary = 0;            // some material reflective != 0 or transparency != 0
     int32_t max_children = 0;             // max secondary rays one shading event queues (0, 1 or 2)
+    int32_t tri_inline = 0;               // every triangle node carries p1/e1/e2 inline (NF_TRI_INLINE)
     int32_t has_csg = 0;
     int32_t has_quad = 0;
     int32_t complex_patterns = 0;         // tree-evaluated patterns (pattern_tree)

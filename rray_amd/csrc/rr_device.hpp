@@ -17,6 +17,9 @@ enum NodeFlags : int32_t {
     NF_IN_CSG = 2,      // inside a CSG subtree: intersected only through the CSG's evaluation
     NF_DIAG = 4,        // inverse is diagonal + translation (scale / translate objects): 3 products per
                         // transform instead of 9 (device_core.inc xf_ray_node)
+    NF_TRI_INLINE = 8,  // triangle with an identity inverse (every OBJ face): inv[0..8] hold its p1, e1, e2
+                        // (DevTri order), so the walk's exact test needs no dependent DevTri load; the
+                        // identity itself is implied by NF_IDENT (also set)
     NF_CSG_LHIT0 = 256, // bit (8 + d): for the CSG at position d of this leaf's ancestor chain,
                         // left.includes(this leaf) (csg.rs:86-88 with Object::includes semantics)
 };
@@ -142,6 +145,7 @@ struct DevScene {
     int32_t general;          // CSGs or cylinders / cones present: the kernels' G = 2 variant
     int32_t lds_culls;        // culls + chunks staged in LDS per workgroup (fits in RR_LDS_CULL_BYTES)
     int32_t complex_patterns; // some pattern is Gradient / Blend / Perturbed / Noise / Texture
+    int32_t tri_inline;       // every triangle node is NF_TRI_INLINE (the walks read p1/e1/e2 from the node)
     int32_t n_free;           // trailing chunks holding one unbounded top-level leaf each (planes): the
                               // last n_free nodes, tested without culling before the chunk passes
     float bs_c[3], bs_r;      // sphere around every bounded node's cull (bs_r < 0: none); rays whose origin

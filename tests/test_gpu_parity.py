@@ -80,6 +80,28 @@ def test_render_matches_oracle(renderer, name, W, H, aa):
     assert got["stats"]["shade_events"] == st["shade_events"]
 
 
+@pytest.mark.parametrize("name,W,H,aa", [("c4_teapot.yaml", 48, 28, 2), ("c4_teapot.yaml", 40, 24, 4),
+                                         ("c2_s1024.yaml", 32, 20, 4), ("c2_s1024.yaml", 16, 10, 8),
+                                         ("c1_readme.yaml", 24, 16, 2)])
+def test_in_wave_aa_average(renderer, name, W, H, aa):
+    """Frames without secondary rays at aa 2 / 4 / 8 with full 8x8 sample tiles: the level-0 waves box-average
+    their own samples (deliver_wave_avg, canvas.rs:85-96 order) and no canvas is written.  The image must
+    equal the oracle's average; with the canvas requested as well, both outputs must match.  (The README
+    scene's glass sphere has secondary rays: the canvas path, for contrast.)"""
+    scene, (o, cam) = _yaml_pair(name, W, H, aa)
+    renderer.upload(scene)
+    got = renderer.render(scene.camera, aa=aa, max_depth=5, seed=7)
+    canvas, st = o.render(cam, max_depth=5, seed=7, threads=0)
+    ref = o.aa_average(canvas, aa)
+    _compare(got["avg"], ref, f"{name} {W}x{H} aa{aa} in-wave avg")
+    both = renderer.render(scene.camera, aa=aa, max_depth=5, seed=7, canvas=True)
+    _compare(both["canvas"], canvas, f"{name} {W}x{H} aa{aa} canvas")
+    # the wave's reduction is exactly canvas.rs's box average of the GPU's own samples
+    assert np.array_equal(both["avg"], got["avg"])
+    assert np.array_equal(got["avg"], o.aa_average(both["canvas"], aa))
+    assert got["stats"]["shade_events"] == st["shade_events"]
+
+
 def test_render_matches_committed_golden(renderer, R):
     """Committed oracle outputs (tests/golden/make_golden.py) — no live oracle needed.  Every config
     scene, C3 and C4 also at their own AA levels (3 and 2)."""
