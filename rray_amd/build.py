@@ -120,17 +120,33 @@ def _compile(src, deps_mtime, verbose):
     return out
 
 
-def build_variant(name, defines, verbose=False):
-    """Experiment build (e.g. RR_STAMPS phase timers) into abtest/<name>/librray_amd.so; select it
-    at run time with RRAY_LIB=<path>.  Never used by the product path."""
+def build_variant(name, defines, verbose=False, patch=None):
+    """Experiment build into abtest/<name>/librray_amd.so; select it at run time with RRAY_EXPERIMENT=1
+    RRAY_LIB=<path>.  Never used by the product path.  patch: a unified diff (tools/patches/*.patch,
+    paths relative to the repo root) applied to a copy of the sources (experiment code such as per-wave
+    phase timers lives there, not in the product sources); defines: extra -D flags."""
+    import shutil
+
     out_dir = os.path.join(ROOT, "abtest", name)  # travels to the GPU box (abtest/ is git-ignored)
     os.makedirs(out_dir, exist_ok=True)
     flags = ["-D" + d for d in defines]
+    csrc = CSRC
+    if patch:
+        src_root = os.path.join(out_dir, "src")
+        shutil.rmtree(src_root, ignore_errors=True)
+        shutil.copytree(os.path.join(ROOT, "rray_amd", "csrc"), os.path.join(src_root, "rray_amd", "csrc"))
+        shutil.copytree(os.path.join(ROOT, "include"), os.path.join(src_root, "include"))
+        r = subprocess.run(["patch", "-p1", "-s", "-d", src_root, "-i", os.path.abspath(patch)], capture_output=True,
+                           text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"patch {patch} failed:\n{r.stdout}{r.stderr}")
+        csrc = os.path.join(src_root, "rray_amd", "csrc")
 
     def one(src):
         o = os.path.join(out_dir, os.path.splitext(src)[0] + ".o")
         pre = [HIPCC, "-x", "hip"] if src.endswith(".cpp") else [HIPCC]
-        cmd = pre + COMMON + DEVICE + flags + ["-c", os.path.join(CSRC, src), "-o", o]
+        inc = ["-I" + os.path.join(os.path.dirname(os.path.dirname(csrc)), "include")] if patch else []
+        cmd = pre + COMMON + inc + DEVICE + flags + ["-c", os.path.join(csrc, src), "-o", o]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -174,7 +190,11 @@ def build(verbose=False, jobs=None):
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 2 and sys.argv[1] == "variant":
-        print(build_variant(sys.argv[2], sys.argv[3:]))
+    if len(sys.argv) > 2 and sys.argv[1] == "variant":  # variant <name> [--patch file] [DEFINE ...]
+        args = sys.argv[3:]
+        patch = None
+        if args[:1] == ["--patch"]:
+            patch, args = args[1], args[2:]
+        print(build_variant(sys.argv[2], args, patch=patch))
     else:
         print(build(verbose="-v" in sys.argv))

@@ -73,6 +73,12 @@ struct CombArgs {
     int64_t hs, lrows;  // lrows > 0: level-0 events are in tile order (tile_to_local)
 };
 
+// The walking kernels' dynamic LDS (render_levels.inc): the scene's culls (when staged), then with <=
+// RR_PRELIT_LIGHTS lights (PRE) every light's prelit terms ([light][6][256] doubles) and the area-light
+// stage (scenes with an area light).
+constexpr int RR_PRELIT_LIGHTS = 2;
+constexpr size_t RR_AREA_STAGE_BYTES = 3 * 256 * 8 + 2 * 256 * 4;
+
 // Level-0 camera events run in 8x8-sample tiles of the part-local supersampled canvas (8-row bands,
 // 8-column tiles inside a band; the last band / column may be narrower) so that a wave's 64 rays
 // form a tight bundle for the culling in walk_nodes.  Maps tile-order index t to the row-major
