@@ -154,7 +154,46 @@ void reorder_spatial(HostScene& hs) {
         key[i] = m;
     }
     auto by_key = [&](int a, int b) { return key[a] < key[b]; };
-    std::stable_sort(top.begin(), top.end(), by_key);
+    // Sibling lists of more than 64 bounded leaves (meshes, sphere fields) are ordered by a recursive
+    // median split instead: along the longest axis of the members' centres, at a multiple of 64 near the
+    // middle, down to buckets of <= 64 — each bucket becomes one chunk (chunk_break), and a bucket of nearby
+    // members has a small bounding sphere.  Morton order sliced every 64 nodes can straddle a cell boundary
+    // and join two distant patches in one chunk.
+    std::vector<char> bucket_start((size_t)N, 0);
+    std::function<void(std::vector<int>&, size_t, size_t)> kd = [&](std::vector<int>& v, size_t b, size_t e) {
+        if (e - b <= 64) {
+            std::stable_sort(v.begin() + b, v.begin() + e, by_key);
+            bucket_start[v[b]] = 1;
+            return;
+        }
+        double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
+        for (size_t q = b; q < e; ++q)
+            for (int k = 0; k < 3; ++k) {
+                mn[k] = std::fmin(mn[k], hs.culls[v[q]].c[k]);
+                mx[k] = std::fmax(mx[k], hs.culls[v[q]].c[k]);
+            }
+        int ax = 0;
+        for (int k = 1; k < 3; ++k)
+            if (mx[k] - mn[k] > mx[ax] - mn[ax]) ax = k;
+        std::stable_sort(v.begin() + b, v.begin() + e, [&](int a, int c) {
+            const float fa = hs.culls[a].c[ax], fc = hs.culls[c].c[ax];
+            return fa < fc || (fa == fc && key[a] < key[c]);
+        });
+        const size_t n = e - b, left = 64 * ((n + 127) / 128);  // a multiple of 64, about half
+        kd(v, b, b + left);
+        kd(v, b + left, e);
+    };
+    auto order = [&](std::vector<int>& v) {
+        size_t nb = 0;
+        bool leaves = true;
+        for (int i : v) {
+            if (std::isfinite(hs.culls[i].r)) ++nb;
+            leaves = leaves && !is_container(hs.nodes[i].kind);
+        }
+        std::stable_sort(v.begin(), v.end(), by_key);  // bounded first (unbounded keys are all-ones)
+        if (leaves && nb > 64) kd(v, 0, nb);
+    };
+    order(top);
     // a CSG concatenates left then right and sorts stably (csg.rs:105-113): its subtree keeps the
     // reference order, so the kernel's in-subtree evaluation order is the reference's
     std::vector<char> in_csg((size_t)N, 0);
@@ -166,7 +205,7 @@ void reorder_spatial(HostScene& hs) {
             }
     for (int i = 0; i < N; ++i) {
         if (in_csg[i]) hs.nodes[i].flags |= NF_IN_CSG;
-        if (hs.nodes[i].kind != RR_CSG && !in_csg[i]) std::stable_sort(kids[i].begin(), kids[i].end(), by_key);
+        if (hs.nodes[i].kind != RR_CSG && !in_csg[i]) order(kids[i]);
     }
     std::vector<int> perm;
     perm.reserve((size_t)N);
@@ -195,6 +234,8 @@ void reorder_spatial(HostScene& hs) {
         if (v >= 0) v = newidx[v];
     hs.nodes.swap(nodes);
     hs.culls.swap(culls);
+    hs.chunk_break.assign((size_t)N, 0);
+    for (int k = 0; k < N; ++k) hs.chunk_break[k] = bucket_start[perm[k]];
 }
 
 // Runs of up to 64 consecutive nodes with a bounding sphere of their culls; unbounded nodes
@@ -213,8 +254,15 @@ void build_chunks(HostScene& hs) {
             continue;
         }
         double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+        // a chunk ends at 64 nodes, before an unbounded node, at a spatial bucket's start, and around a
+        // container (a group's cull spans its whole subtree: in a chunk of its own it does not widen its
+        // children's chunks)
+        auto brk = [&](int m) {
+            return (!hs.chunk_break.empty() && hs.chunk_break[m]) || is_container(hs.nodes[m].kind) ||
+                   is_container(hs.nodes[m - 1].kind);
+        };
         int j = i;
-        for (; j < N && j - i < 64 && std::isfinite(hs.culls[j].r); ++j)
+        for (; j < N && j - i < 64 && std::isfinite(hs.culls[j].r) && (j == i || !brk(j)); ++j)
             for (int k = 0; k < 3; ++k) {
                 lo[k] = std::fmin(lo[k], (double)hs.culls[j].c[k] - hs.culls[j].r);
                 hi[k] = std::fmax(hi[k], (double)hs.culls[j].c[k] + hs.culls[j].r);

@@ -21,6 +21,7 @@ struct HostScene {
     std::vector<DevTexture> textures;
     std::vector<uint32_t> texels;
     std::vector<int32_t> node_of_object;  // object id -> node index (-1 if not in the scene tree)
+    std::vector<char> chunk_break;        // node starts a spatial bucket (reorder_spatial -> build_chunks)
     int32_t has_transparent = 0;
     int32_t has_secondary = 0;            // some material reflective != 0 or transparency != 0
     int32_t max_children = 0;             // max secondary rays one shading event queues (0, 1 or 2)
