@@ -288,33 +288,7 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             A.lcount = lc + d * rr::LC_COUNT;
             A.counters = frame_counters(c, c->epoch);
             A.counters_zero = (c->zero_next && d == 0 && base == 0) ? frame_counters(c, c->epoch ^ 1) : nullptr;
-            A.stamps = nullptr;
-#ifdef RR_STAMPS
-            // experiment builds: per-wave phase timers of level $RRAY_STAMPS_LEVEL (0) of the first batch -> $RRAY_STAMPS
-            const char* stamp_path = std::getenv("RRAY_STAMPS");
-            static DBuf stamp_buf;
-            const size_t stamp_bytes = (size_t)2 * (1 << 16) * 16 * sizeof(unsigned long long);
-            A.stamps = nullptr;
-            const int stamp_level = std::getenv("RRAY_STAMPS_LEVEL") ? std::atoi(std::getenv("RRAY_STAMPS_LEVEL")) : 0;
-            if (stamp_path && d == stamp_level && base == 0) {
-                HIPCHK(stamp_buf.ensure(stamp_bytes));
-                HIPCHK(hipMemsetAsync(stamp_buf.p, 0, stamp_bytes, st));
-                A.stamps = stamp_buf.as<unsigned long long>();
-                A.stamp_stride = std::getenv("RRAY_STAMPS_STRIDE") ? std::max(1, std::atoi(std::getenv("RRAY_STAMPS_STRIDE"))) : 1;
-            }
-#endif
             HIPCHK(rr::launch_level(c->S, A, st, c->profile ? &c->prof : nullptr));
-#ifdef RR_STAMPS
-            if (A.stamps) {
-                std::vector<unsigned long long> hv(stamp_bytes / sizeof(unsigned long long));
-                HIPCHK(hipMemcpyAsync(hv.data(), stamp_buf.p, stamp_bytes, hipMemcpyDeviceToHost, st));
-                HIPCHK(hipStreamSynchronize(st));
-                if (FILE* fp = std::fopen(stamp_path, "wb")) {
-                    std::fwrite(hv.data(), 1, stamp_bytes, fp);
-                    std::fclose(fp);
-                }
-            }
-#endif
         }
         // bottom-up shade_hit sums of the events with children (scene.rs:172-177); fused levels finish
         // their chains in the kernels

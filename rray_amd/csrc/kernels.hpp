@@ -53,8 +53,6 @@ struct LevelArgs {
     int32_t jitter_mode;
     unsigned long long* counters;  // C_* totals
     unsigned long long* counters_zero;  // the next frame's counter buffer, zeroed by this frame's kernels (or null)
-    unsigned long long* stamps;    // RR_STAMPS experiment builds only: per-wave phase timers (else null)
-    int64_t stamp_stride;          // RR_STAMPS: every stamp_stride-th wave is recorded ($RRAY_STAMPS_STRIDE)
 };
 
 struct CombArgs {

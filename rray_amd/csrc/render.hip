@@ -102,10 +102,6 @@ bool fused_levels(const DevScene& S) { return !S.has_transparent && !std::getenv
 hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t st, KernelProf* prof) {
     if (A.n <= 0) return hipSuccess;
     const int g = S.general ? 2 : S.has_groups ? 1 : 0;  // G: flat / groups / general (CSG, 4-entry leaves)
-#ifdef RR_QUICK  // experiment builds: only the flat, LDS-culled, simple-pattern kernels (fast compiles)
-    if (g != 0 || !S.lds_culls || S.complex_patterns) return hipErrorNotSupported;
-    launch_level_t<0, true>(S, A, st, prof);
-#else
     if (g == 2) {
         if (S.lds_culls)
             launch_level_t<2, true>(S, A, st, prof);
@@ -122,7 +118,6 @@ hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t st, K
         else
             launch_level_t<0, false>(S, A, st, prof);
     }
-#endif
     return hipGetLastError();
 }
 

@@ -7,10 +7,8 @@
 #include "wavefront.hpp"
 
 namespace rr {
-#ifndef RR_QUICK  // experiment builds keep only the flat, LDS-culled kernels
 #include "render_common.inc"
 #include "render_levels.inc"
 
 template void launch_level_t<1, false>(const DevScene&, const LevelArgs&, hipStream_t, KernelProf*);
-#endif
 }  // namespace rr

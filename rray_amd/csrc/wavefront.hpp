@@ -57,10 +57,7 @@ enum { CF_HIT = 1, CF_REFRACT_CHILD = 2 };
 // (block b appends to segment b % RR_NSEG with one atomic per wave, no workgroup barrier; the next
 // level's block b reads segment b % RR_NSEG — blocks are dealt to the XCDs round-robin, so a segment's
 // producer and consumer run on the same XCD); LC_SEG0 + s counts segment s of the level.
-#ifndef RR_NSEG_N
-#define RR_NSEG_N 1024
-#endif
-constexpr int RR_NSEG = RR_NSEG_N;
+constexpr int RR_NSEG = 1024;
 enum { LC_CHILDREN = 0, LC_PENDING, LC_N1N2, LC_SEG0, LC_COUNT = LC_SEG0 + RR_NSEG };
 
 }  // namespace rr

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Experiment: per-wave phase timers (RR_STAMPS build) for the bench workload's level-0 kernel.
+# Experiment: per-wave phase timers for the bench workload's level-0 kernel.  Build the variant first:
+#   python rray_amd/build.py variant stamps --patch tools/patches/stamps.patch RR_STAMPS
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
