@@ -42,6 +42,7 @@ struct LevelArgs {
     ChainRec* chain[RR_MAX_DEPTH + 1];  // FUSED levels: each level's pending surface sums (in the comb buffers)
     double* out;             // level 0: canvas / color_at results (3 doubles per local sample), or null
     void* avg;               // aa == 1: the averaged image written directly (canvas.rs:85-96 with aa = 1)
+    int32_t pad_children;    // fused levels: children in per-wave 64-slot blocks (holes: Event.parent == -2)
     int32_t aa_wave;         // 2 / 4 / 8: every pixel's aa x aa samples lie in one wave's 8x8 tile and no
                              // sample has a secondary ray: the wave box-averages and writes avg (0: off)
     int32_t avg_f32;         // avg holds floats (RR_OUT_AVG_F32)
