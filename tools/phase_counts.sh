@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOTDIR=$(pwd)
 export TMPDIR=/tmp RRAY_EXPERIMENT=1 RRAY_LIB=$ROOTDIR/abtest/phase/librray_amd.so
 WL=${WL:-c2_s1024}
-for k in 1 2 3 4 5 0; do
+for k in ${KS:-1 2 3 4 5 0}; do
   OUT=$ROOTDIR/gpurun_out/phase_$WL/k$k
   mkdir -p "$OUT"
   (cd /tmp && RRAY_PHASE_EXIT=$k timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM \
@@ -17,10 +17,10 @@ for k in 1 2 3 4 5 0; do
      echo "k=$k failed"; tail -5 "$OUT.log"; exit 1; }
 done
 python3 - "$WL" <<'PY'
-import csv, collections, glob, sys
+import csv, collections, glob, os, sys
 wl = sys.argv[1]
 prev = None
-for k in [1, 2, 3, 4, 5, 0]:
+for k in [int(x) for x in os.environ.get("KS", "1 2 3 4 5 0").split()]:
     f = glob.glob(f"gpurun_out/phase_{wl}/k{k}/**/run_counter_collection.csv", recursive=True)[0]
     per = collections.defaultdict(collections.Counter)
     for r in csv.DictReader(open(f)):
