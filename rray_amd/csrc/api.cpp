@@ -72,6 +72,14 @@ struct rr_ctx {
     DBuf culls, chunks, nodes, groups, shapes, tris, mats, pats, lights, textures, texels;
     // workspace
     DBuf counters, lcount, hit, n12, n1n2, ev_a, ev_b, canvas, rays0, qout;
+    // per-tile camera-ray bundles of the last camera / part layout (tile_bundle_kernel), reused while they match
+    DBuf tiles;
+    struct TileKey {
+        rr::DevCamera cam;
+        int64_t hs, lrows;
+        int32_t aa, part, nparts, block_rows;
+    } tile_key{};
+    bool tiles_valid = false;
     std::vector<DBuf> comb, comb_ext, pend;  // one per level (comb_ext: scenes with transparency)
     unsigned long long* h_counters = nullptr;
     // counters: [frame buffer 0][frame buffer 1][queries]; frames alternate (`epoch`), and each
@@ -199,6 +207,50 @@ LevelPlan plan_levels(int64_t nb, int k, int max_depth, bool ext, bool fused = f
     return p;
 }
 
+// level-0 index math: magic divisors, and the wave-uniform tile path when every tile is a full 8x8 and the
+// batch starts on a tile boundary
+void set_level0_index(rr::LevelArgs& A) {
+    A.aa_magic = A.aa > 1 ? (uint32_t)((1ull << 32) / (uint64_t)A.aa) : 0u;
+    A.br_magic = A.block_rows > 1 ? (uint32_t)((1ull << 32) / (uint64_t)A.block_rows) : 0u;
+    A.tile_fast = !A.rays0 && A.lrows > 0 && A.hs % 8 == 0 && A.lrows % 8 == 0 && A.base % 64 == 0 ? 1 : 0;
+    A.tiles_per_row = (uint32_t)(A.hs / 8);
+}
+
+// The per-tile camera bundles of this render's part (tile_bundle_kernel), recomputed only when the camera or
+// the part layout changed since the last render on this context.  Null when the tiles are not all full 8x8
+// or the camera is not affine (the walks build their bundles themselves then).
+int tile_bundles(rr_ctx* c, const rr::LevelArgs& base_args, hipStream_t st, const float** out) {
+    *out = nullptr;
+    rr::LevelArgs T = base_args;
+    T.base = 0;
+    T.level = 0;
+    set_level0_index(T);
+    if (!T.tile_fast || !T.cam_affine) return RR_OK;
+    // few-node flat scenes with LDS culls walk node by node without bundles (walk_nodes)
+    if (!c->S.has_groups && !c->S.general && c->S.lds_culls && c->S.n_nodes <= rr::RR_BUNDLE_MIN_NODES) return RR_OK;
+    const int64_t n_tiles = T.hs * T.lrows / 64;
+    const size_t want = (size_t)n_tiles * rr::RR_TILE_BUNDLE_FLOATS * sizeof(float);
+    if (want > c->tiles.bytes) {
+        HIPCHK(c->tiles.ensure(want));
+        c->tiles_valid = false;
+    }
+    rr_ctx::TileKey key{};
+    key.cam = T.cam;
+    key.hs = T.hs;
+    key.lrows = T.lrows;
+    key.aa = T.aa;
+    key.part = T.part;
+    key.nparts = T.nparts;
+    key.block_rows = T.block_rows;
+    if (!c->tiles_valid || std::memcmp(&key, &c->tile_key, sizeof key) != 0) {
+        HIPCHK(rr::launch_tile_bundles(c->S, T, c->tiles.as<float>(), n_tiles, st));
+        c->tile_key = key;
+        c->tiles_valid = true;
+    }
+    *out = c->tiles.as<float>();
+    return RR_OK;
+}
+
 // The averaged image can be written by the level-0 waves themselves (deliver_wave_avg) when every
 // pixel's samples lie in one wave's 8x8 tile (aa in {2, 4, 8}, full tiles: the tile_fast layout) and no
 // sample spawns a secondary ray (fused levels with no reflective / transparent material, or depth 0).
@@ -250,12 +302,7 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             const bool children_possible = d + 1 < p.levels;
             rr::LevelArgs A = base_args;
             A.base = base;
-            // level-0 index math: magic divisors, and the wave-uniform tile path when every tile is
-            // a full 8x8 and this batch starts on a tile boundary
-            A.aa_magic = A.aa > 1 ? (uint32_t)((1ull << 32) / (uint64_t)A.aa) : 0u;
-            A.br_magic = A.block_rows > 1 ? (uint32_t)((1ull << 32) / (uint64_t)A.block_rows) : 0u;
-            A.tile_fast = !A.rays0 && A.lrows > 0 && A.hs % 8 == 0 && A.lrows % 8 == 0 && base % 64 == 0 ? 1 : 0;
-            A.tiles_per_row = (uint32_t)(A.hs / 8);
+            set_level0_index(A);
             A.level = d;
             A.rem = max_depth - d;
             A.n = p.cap[d];
@@ -490,7 +537,7 @@ void rr_destroy(rr_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)sync_ctx(c);
     for (DBuf* b : {&c->culls, &c->chunks, &c->nodes, &c->groups, &c->shapes, &c->tris, &c->mats, &c->pats, &c->lights, &c->textures, &c->texels, &c->counters,
-                    &c->lcount, &c->hit, &c->n12, &c->n1n2, &c->ev_a, &c->ev_b, &c->canvas, &c->rays0, &c->qout})
+                    &c->lcount, &c->hit, &c->n12, &c->n1n2, &c->ev_a, &c->ev_b, &c->canvas, &c->rays0, &c->qout, &c->tiles})
         b->release();
     for (auto& b : c->comb) b.release();
     for (auto& b : c->comb_ext) b.release();
@@ -722,6 +769,8 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     A.seed = o->seed;
     A.jitter_mode = o->jitter_mode;
     const int32_t f32 = (o->flags & RR_OUT_AVG_F32) ? 1 : 0;
+    rc = tile_bundles(c, A, st, &A.tile_bundles);
+    if (rc != RR_OK) return rc;
     c->zero_next = true;
     rc = run_levels(c, A, total, o->max_depth, canvas, st, direct_avg ? d_avg : nullptr, f32, wave_avg ? o->aa : 0);
     c->zero_next = false;

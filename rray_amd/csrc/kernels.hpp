@@ -42,6 +42,8 @@ struct LevelArgs {
     ChainRec* chain[RR_MAX_DEPTH + 1];  // FUSED levels: each level's pending surface sums (in the comb buffers)
     double* out;             // level 0: canvas / color_at results (3 doubles per local sample), or null
     void* avg;               // aa == 1: the averaged image written directly (canvas.rs:85-96 with aa = 1)
+    const float* tile_bundles;  // level 0, tile_fast, affine camera: per-tile camera-ray bundles (tile_bundle_kernel,
+                                // RR_TILE_BUNDLE_FLOATS each, indexed by tile), or null: built in the walk
     int32_t pad_children;    // fused levels: children in per-wave 64-slot blocks (holes: Event.parent == -2)
     int32_t aa_wave;         // 2 / 4 / 8: every pixel's aa x aa samples lie in one wave's 8x8 tile and no
                              // sample has a secondary ray: the wave box-averages and writes avg (0: off)
@@ -119,6 +121,10 @@ struct KernelProf {
 };
 
 hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t stream, KernelProf* prof = nullptr);
+// One camera-ray bundle per full 8x8 tile of the part (A: level-0 tile_fast arguments of the whole part), into
+// out (n_tiles x RR_TILE_BUNDLE_FLOATS floats): exactly the bundle make_bundle's cam_tile path builds in the walk.
+constexpr int RR_TILE_BUNDLE_FLOATS = 12;
+hipError_t launch_tile_bundles(const DevScene& S, const LevelArgs& A, float* out, int64_t n_tiles, hipStream_t stream);
 // trace + shade run as one kernel per level (no transparent material, so no n1/n2 walk between them);
 // those levels finish their reflection chains themselves and need no combine pass
 bool fused_levels(const DevScene& S);

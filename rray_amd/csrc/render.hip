@@ -87,6 +87,45 @@ __global__ void __launch_bounds__(256) shadow_query_kernel(DevScene S, const dou
 }
 
 
+// One thread per full 8x8 tile of the part: its four corner camera rays exactly as the level-0 lanes compute
+// them (level0_px + camera_ray, then f32), and the tile's bundle from them (cam_corner_bundle).  Run once per
+// camera / part layout (the context caches the table), so the level-0 walks read their bundle instead of
+// building it (~100 VALU per wave).
+__global__ void __launch_bounds__(256) tile_bundle_kernel(LevelArgs A, float* __restrict__ out, int64_t n_tiles) {
+    const int64_t T = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (T >= n_tiles) return;
+    const int corner[4] = {0, 7, 56, 63};
+    float o[3] = {0.0f, 0.0f, 0.0f}, dc[4][3];
+    for (int j = 0; j < 4; ++j) {
+        const Px0 q = level0_px<false>(A, T * 64 + corner[j]);
+        const Ray r = camera_ray(A.cam, A.cam_affine, q.px, q.py);
+        o[0] = (float)r.o.x;
+        o[1] = (float)r.o.y;
+        o[2] = (float)r.o.z;
+        dc[j][0] = (float)r.d.x;
+        dc[j][1] = (float)r.d.y;
+        dc[j][2] = (float)r.d.z;
+    }
+    const Bundle B = cam_corner_bundle(o, dc);
+    float* p = out + T * RR_TILE_BUNDLE_FLOATS;
+    for (int k = 0; k < 3; ++k) {
+        p[k] = B.o[k];
+        p[3 + k] = B.a[k];
+    }
+    p[6] = B.rho;
+    p[7] = B.tanT;
+    p[8] = B.secT;
+    p[9] = __int_as_float(B.ok);
+    p[10] = p[11] = 0.0f;
+}
+
+hipError_t launch_tile_bundles(const DevScene& S, const LevelArgs& A, float* out, int64_t n_tiles, hipStream_t st) {
+    (void)S;
+    if (n_tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tile_bundle_kernel, dim3(blocks_for(n_tiles)), dim3(256), 0, st, A, out, n_tiles);
+    return hipGetLastError();
+}
+
 hipEvent_t KernelProf::get() {
     if (used == pool.size()) {
         hipEvent_t e = nullptr;
