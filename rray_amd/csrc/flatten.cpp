@@ -755,6 +755,17 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
         ++n_inline;
     }
     out.tri_inline = n_tri > 0 && n_inline == n_tri ? 1 : 0;
+    for (DevChunk& ch : out.chunks) {  // mesh runs (DevChunk.tri_parent)
+        ch.tri_parent = -2;
+        const DevNode& a = out.nodes[ch.start];
+        bool run = a.parent >= 0;
+        for (int m = ch.start; run && m < ch.start + ch.count; ++m) {
+            const DevNode& nd = out.nodes[m];
+            run = (nd.kind == RR_TRIANGLE || nd.kind == RR_SMOOTH_TRIANGLE) && (nd.flags & NF_TRI_INLINE) &&
+                  !(nd.flags & NF_IN_CSG) && nd.parent == a.parent;
+        }
+        if (run) ch.tri_parent = a.parent;
+    }
     return RR_OK;
 }
 

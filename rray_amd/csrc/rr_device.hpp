@@ -119,10 +119,13 @@ struct alignas(16) DevCull {
 };
 
 // A run of consecutive nodes (<= 64) with the world-space bounding sphere of their culls.
+// tri_parent >= 0: every node of the chunk is a triangle with its data inline (NF_TRI_INLINE), outside any
+// CSG, and a child of node tri_parent (a mesh's run): the walks test it without per-node kind / transform
+// dispatch (walk_nodes); -2: none of that holds.
 struct alignas(16) DevChunk {
     DevCull cull;
     int32_t start, count;
-    int32_t pad0, pad1;
+    int32_t tri_parent, pad1;
 };
 
 struct DevScene {
