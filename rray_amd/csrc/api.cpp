@@ -589,6 +589,11 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
             break;
         ++S.n_free;
     }
+    S.free_planes = 1;
+    for (int k = 0; k < S.n_free; ++k) {
+        const rr::DevNode& nd = c->host.nodes[c->host.nodes.size() - 1 - k];
+        if (nd.kind != RR_PLANE || !(nd.flags & rr::NF_IDENT)) S.free_planes = 0;
+    }
     S.nodes = c->nodes.as<rr::DevNode>();
     S.groups = c->groups.as<rr::DevGroup>();
     S.shapes = c->shapes.as<rr::DevShape>();

@@ -755,16 +755,22 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
         ++n_inline;
     }
     out.tri_inline = n_tri > 0 && n_inline == n_tri ? 1 : 0;
-    for (DevChunk& ch : out.chunks) {  // mesh runs (DevChunk.tri_parent)
-        ch.tri_parent = -2;
+    for (DevChunk& ch : out.chunks) {  // runs of one kind (DevChunk.run)
+        ch.run = CR_NONE;
         const DevNode& a = out.nodes[ch.start];
-        bool run = a.parent >= 0;
-        for (int m = ch.start; run && m < ch.start + ch.count; ++m) {
+        bool mesh = a.parent >= 0, spheres = true;
+        for (int m = ch.start; m < ch.start + ch.count; ++m) {
             const DevNode& nd = out.nodes[m];
-            run = (nd.kind == RR_TRIANGLE || nd.kind == RR_SMOOTH_TRIANGLE) && (nd.flags & NF_TRI_INLINE) &&
-                  !(nd.flags & NF_IN_CSG) && nd.parent == a.parent;
+            mesh = mesh && (nd.kind == RR_TRIANGLE || nd.kind == RR_SMOOTH_TRIANGLE) && (nd.flags & NF_TRI_INLINE) &&
+                   !(nd.flags & NF_IN_CSG) && nd.parent == a.parent;
+            spheres = spheres && nd.kind == RR_SPHERE && nd.parent < 0 && (nd.flags & NF_DIAG) && !(nd.flags & NF_IDENT) &&
+                      !(nd.flags & NF_IN_CSG);
         }
-        if (run) ch.tri_parent = a.parent;
+        if (mesh) {
+            ch.run = a.parent;
+        } else if (spheres) {
+            ch.run = CR_SPHERE_DIAG;
+        }
     }
     return RR_OK;
 }

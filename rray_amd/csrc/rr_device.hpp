@@ -119,13 +119,15 @@ struct alignas(16) DevCull {
 };
 
 // A run of consecutive nodes (<= 64) with the world-space bounding sphere of their culls.
-// tri_parent >= 0: every node of the chunk is a triangle with its data inline (NF_TRI_INLINE), outside any
-// CSG, and a child of node tri_parent (a mesh's run): the walks test it without per-node kind / transform
-// dispatch (walk_nodes); -2: none of that holds.
+// Runs of one kind, which the walks test without per-node kind / flag / transform dispatch (walk_nodes):
+// run >= 0: every node is a triangle with its data inline (NF_TRI_INLINE), outside any CSG, and a child of node
+// `run` (a mesh); CR_SPHERE_DIAG: every node is a top-level sphere with a diagonal inverse (NF_DIAG).  One field,
+// so the walks read one value per chunk.
+enum ChunkRun : int32_t { CR_NONE = -1, CR_SPHERE_DIAG = -2 };
 struct alignas(16) DevChunk {
     DevCull cull;
     int32_t start, count;
-    int32_t tri_parent, pad1;
+    int32_t run, pad;
 };
 
 struct DevScene {
@@ -151,6 +153,7 @@ struct DevScene {
     int32_t tri_inline;       // every triangle node is NF_TRI_INLINE (the walks read p1/e1/e2 from the node)
     int32_t n_free;           // trailing chunks holding one unbounded top-level leaf each (planes): the
                               // last n_free nodes, tested without culling before the chunk passes
+    int32_t free_planes;      // every one of them is a plane with an identity inverse (no dispatch in the walks)
     float bs_c[3], bs_r;      // sphere around every bounded node's cull (bs_r < 0: none); rays whose origin
                               // lies far outside it are culled from a point nearer to it (make_bundle)
 };
