@@ -20,13 +20,13 @@ def short(name):
 
 def frames(rows, key):
     """Label each rr:: dispatch with (short name, occurrence index inside its frame).  A frame starts at
-    each dispatch of the first rr:: kernel seen."""
+    each dispatch of the first rr:: kernel seen (other than the once-per-camera tile_bundle_kernel)."""
     out, first, seen = [], None, collections.Counter()
     for r in rows:
         k = short(r["Kernel_Name"])
         if not k:
             continue
-        if first is None:
+        if first is None and k != "tile_bundle_kernel":  # bundles: once per camera, not per frame
             first = k
         if k == first:
             seen = collections.Counter()
