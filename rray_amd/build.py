@@ -26,7 +26,7 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "
           "-I" + os.path.join(ROOT, "include")]
 DEVICE = ["--offload-arch=" + ARCH, "-mllvm", "-disable-promote-alloca-to-lds"]
 LEVEL_UNITS = [f"render_levels_g{g}_{lc}.hip" for g in (2, 1, 0) for lc in ("lds", "gl")]  # slowest first
-SOURCES = LEVEL_UNITS + ["render.hip", "api.cpp", "multi.cpp", "flatten.cpp", "frontend.cpp", "yaml.cpp", "png.cpp"]
+SOURCES = LEVEL_UNITS + ["render.hip", "api.cpp", "multi.cpp", "flatten.cpp", "frontend.cpp", "yaml.cpp", "png.cpp", "jpeg.cpp"]
 
 
 def source_digest():

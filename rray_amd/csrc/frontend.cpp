@@ -219,7 +219,7 @@ struct Builder {
         std::vector<uint8_t> rgba;
         uint32_t w = 0, h = 0;
         std::string err;
-        int rc = rr::read_png_rgba(path, rgba, w, h, err);
+        int rc = rr::read_image_rgba(path, rgba, w, h, err);
         if (rc != RR_OK) panic(err, rc);
         if (w > 0x7fffffffu || h > 0x7fffffffu) panic(path + ": texture too large", RR_E_LIMIT);
         int id = (int)(S.tex_size.size() / 2);

@@ -36,7 +36,7 @@ int paeth(int a, int b, int c) {
 }
 }  // namespace
 
-int read_png_rgba(const std::string& path, std::vector<uint8_t>& rgba, uint32_t& width, uint32_t& height,
+int read_image_rgba(const std::string& path, std::vector<uint8_t>& rgba, uint32_t& width, uint32_t& height,
                   std::string& err) {
     FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) {
@@ -48,9 +48,14 @@ int read_png_rgba(const std::string& path, std::vector<uint8_t>& rgba, uint32_t&
     size_t n;
     while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) file.insert(file.end(), buf, buf + n);
     std::fclose(f);
+    if (file.size() >= 3 && file[0] == 0xFF && file[1] == 0xD8 && file[2] == 0xFF) {
+        int rc = decode_jpeg_rgba(file.data(), file.size(), rgba, width, height, err);
+        if (rc != RR_OK) err = path + ": " + err;
+        return rc;
+    }
     static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
     if (file.size() < 8 || std::memcmp(file.data(), sig, 8) != 0) {
-        err = path + ": not a PNG file (other image formats need a host-side decoder: pass texels in rr_scene_desc)";
+        err = path + ": neither PNG nor JPEG (other image formats need a host-side decoder: pass texels in rr_scene_desc)";
         return RR_E_LIMIT;
     }
     uint32_t w = 0, h = 0;

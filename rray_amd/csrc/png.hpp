@@ -7,9 +7,12 @@
 
 namespace rr {
 bool write_png_rgba(const char* path, const uint8_t* rgba, uint32_t width, uint32_t height);
-// 8-bit grey / grey+alpha / RGB / RGBA and 1-8 bit palette or grey, non-interlaced; rows top to
-// bottom as RGBA8.  Returns RR_OK, RR_E_IO (unreadable / corrupt) or RR_E_LIMIT (16-bit or
-// interlaced: outside this decoder).
-int read_png_rgba(const std::string& path, std::vector<uint8_t>& rgba, uint32_t& width, uint32_t& height,
+// Texture file -> RGBA8 rows top to bottom.  PNG: 8-bit grey / grey+alpha / RGB / RGBA and 1-8 bit
+// palette or grey, non-interlaced; JPEG: baseline / extended sequential (jpeg.cpp).  Returns RR_OK,
+// RR_E_IO (unreadable / corrupt) or RR_E_LIMIT (a layout outside these decoders).
+int read_image_rgba(const std::string& path, std::vector<uint8_t>& rgba, uint32_t& width, uint32_t& height,
                   std::string& err);
+// jpeg.cpp: the JPEG decoder on a file's bytes
+int decode_jpeg_rgba(const uint8_t* data, size_t len, std::vector<uint8_t>& rgba, uint32_t& width,
+                     uint32_t& height, std::string& err);
 }

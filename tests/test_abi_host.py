@@ -63,7 +63,7 @@ YAMLS = [(SCENES, f) for f in ("c1_readme.yaml", "c2_s1024.yaml", "c3_s1024_refl
                                "objects_cone.yaml", "shapes_csg.yaml", "shapes_glass.yaml", "shapes_mixed.yaml",
                                "noise_pattern.yaml", "perturbed_pattern.yaml", "objects_sphere.yaml",
                                "objects_cube.yaml", "patterns_noise_mix.yaml", "textures_mix.yaml",
-                               "shapes_torus.yaml")] + [(os.path.join(GOLDEN, "example1"), "example1.yaml")]
+                               "shapes_torus.yaml")] + [(os.path.join(GOLDEN, "example1"), f) for f in ("example1.yaml", "torus.yaml")]
 
 
 @pytest.mark.parametrize("root,name", YAMLS)

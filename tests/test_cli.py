@@ -100,3 +100,25 @@ def test_cli_missing_scene_file_fails(tmp_path):
     assert r.returncode == 1
     assert "rray:" in r.stderr
     assert not (tmp_path / "o.png").exists()
+
+
+@pytest.mark.gpu
+def test_cli_renders_torus_jpeg_scene(tmp_path):
+    """`rray -s torus.yaml` (examples/objects/torus.yaml: JPEG texture) from the scene's directory:
+    the PNG equals the oracle's render (PIL-decoded texture) after `as u8` (canvas.rs:98-105)."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    from oracle.scene_yaml import build_from_yaml
+
+    root = os.path.join(GOLDEN, "example1")
+    out = tmp_path / "torus.png"
+    r = _run(["-W", "200", "-H", "100", "-s", "torus.yaml", "-o", str(out), "-a", "1"], cwd=root)
+    assert r.returncode == 0, r.stderr
+    o, cam = build_from_yaml(open(os.path.join(root, "torus.yaml")).read(), 200, 100, 1, obj_root=root)
+    canvas, _ = o.render(cam, max_depth=5)
+    ref = np.clip(o.aa_average(canvas, 1) * 255.0, 0, 255).astype(np.uint8)  # f64 as u8 saturates
+    got = _png(out)
+    diff = int((got != ref).any(axis=2).sum())
+    print(f"CLI torus.yaml: {diff} of {got.shape[0] * got.shape[1]} pixels differ from the oracle")
+    assert diff == 0

@@ -150,6 +150,21 @@ def test_shape_scenes(renderer, name, W, H, aa):
     assert got["stats"]["shade_events"] == st["shade_events"]
 
 
+@pytest.mark.parametrize("W,H,aa", [(160, 80, 2), (400, 200, 1)])
+def test_torus_jpeg_texture_scene(renderer, W, H, aa):
+    """The reference's examples/objects/torus.yaml: a torus with the JPEG texture
+    examples/Texturelabs_Stone_138M.jpg (texture.rs:15-19), decoded by the product front-end
+    (jpeg.cpp) and by PIL in the oracle; canvas, average and counters bit-compared."""
+    root = os.path.join(GOLDEN, "example1")
+    scene, (o, cam) = _yaml_pair("torus.yaml", W, H, aa, obj_root=root, path=os.path.join(root, "torus.yaml"))
+    renderer.upload(scene)
+    got = renderer.render(scene.camera, aa=aa, max_depth=5, canvas=True)
+    canvas, st = o.render(cam, max_depth=5)
+    _compare(got["canvas"], canvas, "torus.yaml canvas")
+    assert np.array_equal(got["avg"], o.aa_average(canvas, aa))
+    assert got["stats"]["shade_events"] == st["shade_events"]
+
+
 @pytest.mark.parametrize("name,png,aa", [("objects_cylinder.yaml", "objects_cylinder.png", 3),
                                          ("objects_cone.yaml", "objects_cone.png", 3),
                                          ("objects_sphere.yaml", "objects_sphere.png", 3),
