@@ -809,7 +809,7 @@ int rr_render_gather_device(rr_ctx* c, const rr_camera* cam, const rr_render_opt
 int rr_kernel_profile(rr_ctx* c, int enable) {
     rr::DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!c) return fail(RR_E_ARG, "null context");
-    if (c->group) return rr_kernel_profile(rr::group_local(c->group, 0), enable);
+    if (c->group) return rr::group_kernel_profile(c->group, enable);
     HIPCHK(sync_ctx(c));
     int rc = resolve_prof(c);
     if (rc != RR_OK) return rc;
@@ -824,7 +824,7 @@ int rr_kernel_profile(rr_ctx* c, int enable) {
 int rr_kernel_times(rr_ctx* c, double* ms, uint64_t* launches, int32_t n) {
     rr::DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!c) return fail(RR_E_ARG, "null context");
-    if (c->group) return rr_kernel_times(rr::group_local(c->group, 0), ms, launches, n);
+    if (c->group) return rr::group_kernel_times(c->group, ms, launches, n);
     HIPCHK(sync_ctx(c));
     int rc = resolve_prof(c);
     if (rc != RR_OK) return rc;

@@ -6,7 +6,10 @@
 // the largest part's row count; one ncclGather (RCCL over xGMI) brings the tiles to rank 0, whose
 // own tile is rendered in place into the gather buffer, and a small kernel un-interleaves them into
 // frame order.  Two tile buffers alternate so that rendering frame k+1 overlaps the gather of frame
-// k: a render waits only for the gather that last read its buffer.
+// k: a render waits only for the gather that last read its buffer.  Each part also alternates between
+// two render contexts (scene copy + level workspace) on two render streams, so frame k+1's camera level
+// runs beside frame k's deep levels, whose few incoherent waves leave the GPU mostly idle (with a row
+// tile of C3 per GPU the deep levels are a latency floor per frame, tools/part_scaling.py).
 //
 // Two shapes of the same group: rr_create_multi (this process drives n devices, ncclCommInitAll,
 // ncclGroupStart/End around the per-device gathers) and rr_create_rank (one process per GPU,
@@ -88,16 +91,18 @@ hipError_t launch_unshuffle(const double* in, double* out, int64_t W, int64_t H,
 struct rr_group {
     int nranks = 1, rank0 = 0;
     std::vector<int> devices;
-    std::vector<rr_ctx*> subs;
+    std::vector<rr_ctx*> subs[2];         // per local part: frame k renders on subs[k % 2] / render_st[k % 2]
     std::vector<ncclComm_t> comms;
-    std::vector<hipStream_t> render_st, comm_st;
+    std::vector<hipStream_t> render_st[2], comm_st;
     std::vector<hipEvent_t> ev_rendered[2], ev_gathered[2];
     bool virt = false;                    // rr_create_virtual: every part on one device, gather = local copies
     hipEvent_t ev_caller = nullptr;       // root: the caller's stream position at the gather call
     std::vector<DevMem> tile[2];          // non-root local parts: their tile; root: unused
     DevMem recv[2];                       // root: nranks x padded tile (slot 0 = its own tile, in place)
     DevMem frame;                         // root: assembled frame for the blocking rr_render
-    int64_t k = 0;                        // frames issued (buffer = k % 2)
+    int64_t k = 0;                        // frames issued (buffer and render context = k % 2)
+    int nlocal() const { return (int)devices.size(); }
+    int last() const { return k > 0 ? (int)((k - 1) & 1) : 0; }  // the set that rendered the latest frame
     bool root_here() const { return rank0 == 0; }
     // the stream that gathers part l's tile (and releases its buffer): its own comm stream, or for a
     // virtual group root's, where the copies into the receive buffer run
@@ -108,19 +113,21 @@ namespace rr {
 
 static int group_setup(rr_group* g) {
     const int n = (int)g->devices.size();
-    g->subs.assign(n, nullptr);
-    g->render_st.assign(n, nullptr);
     g->comm_st.assign(n, nullptr);
     for (int b = 0; b < 2; ++b) {
+        g->subs[b].assign(n, nullptr);
+        g->render_st[b].assign(n, nullptr);
         g->ev_rendered[b].assign(n, nullptr);
         g->ev_gathered[b].assign(n, nullptr);
         g->tile[b].resize(n);
     }
     for (int l = 0; l < n; ++l) {
-        int rc = rr_create(g->devices[l], &g->subs[l]);
-        if (rc != RR_OK) return rc;
+        for (int b = 0; b < 2; ++b) {
+            int rc = rr_create(g->devices[l], &g->subs[b][l]);
+            if (rc != RR_OK) return rc;
+        }
         GHIP(hipSetDevice(g->devices[l]));
-        GHIP(hipStreamCreateWithFlags(&g->render_st[l], hipStreamNonBlocking));
+        for (int b = 0; b < 2; ++b) GHIP(hipStreamCreateWithFlags(&g->render_st[b][l], hipStreamNonBlocking));
         GHIP(hipStreamCreateWithFlags(&g->comm_st[l], hipStreamNonBlocking));
         for (int b = 0; b < 2; ++b) {
             GHIP(hipEventCreateWithFlags(&g->ev_rendered[b][l], hipEventDisableTiming));
@@ -224,7 +231,8 @@ void group_destroy(rr_group* g) {
     if (!g) return;
     for (size_t l = 0; l < g->devices.size(); ++l) {
         (void)hipSetDevice(g->devices[l]);
-        if (l < g->render_st.size() && g->render_st[l]) (void)hipStreamSynchronize(g->render_st[l]);
+        for (int b = 0; b < 2; ++b)
+            if (l < g->render_st[b].size() && g->render_st[b][l]) (void)hipStreamSynchronize(g->render_st[b][l]);
         if (l < g->comm_st.size() && g->comm_st[l]) (void)hipStreamSynchronize(g->comm_st[l]);
     }
     for (ncclComm_t c : g->comms)
@@ -236,7 +244,8 @@ void group_destroy(rr_group* g) {
             if (l < g->ev_rendered[b].size() && g->ev_rendered[b][l]) (void)hipEventDestroy(g->ev_rendered[b][l]);
             if (l < g->ev_gathered[b].size() && g->ev_gathered[b][l]) (void)hipEventDestroy(g->ev_gathered[b][l]);
         }
-        if (l < g->render_st.size() && g->render_st[l]) (void)hipStreamDestroy(g->render_st[l]);
+        for (int b = 0; b < 2; ++b)
+            if (l < g->render_st[b].size() && g->render_st[b][l]) (void)hipStreamDestroy(g->render_st[b][l]);
         if (l < g->comm_st.size() && g->comm_st[l]) (void)hipStreamDestroy(g->comm_st[l]);
         if (l == 0 && g->root_here()) {
             for (int b = 0; b < 2; ++b) g->recv[b].release();
@@ -244,19 +253,22 @@ void group_destroy(rr_group* g) {
             if (g->ev_caller) (void)hipEventDestroy(g->ev_caller);
         }
     }
-    for (rr_ctx* s : g->subs)
-        if (s) rr_destroy(s);
+    for (int b = 0; b < 2; ++b)
+        for (rr_ctx* s : g->subs[b])
+            if (s) rr_destroy(s);
     delete g;
 }
 
 int group_upload(rr_group* g, const rr_scene_desc* d) {
     DeviceGuard device_guard;
-    for (size_t l = 0; l < g->subs.size(); ++l) {  // the scene is replicated to every device (<= a few MB)
+    for (int l = 0; l < g->nlocal(); ++l) {  // the scene is replicated to every device (<= a few MB), per render context
         GHIP(hipSetDevice(g->devices[l]));
-        GHIP(hipStreamSynchronize(g->render_st[l]));
+        for (int b = 0; b < 2; ++b) GHIP(hipStreamSynchronize(g->render_st[b][l]));
         GHIP(hipStreamSynchronize(g->comm_st[l]));
-        int rc = rr_scene_upload(g->subs[l], d);
-        if (rc != RR_OK) return rc;
+        for (int b = 0; b < 2; ++b) {
+            int rc = rr_scene_upload(g->subs[b][l], d);
+            if (rc != RR_OK) return rc;
+        }
     }
     return RR_OK;
 }
@@ -276,7 +288,7 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
     const int64_t max_rows = gather_tile_rows(H, g->nranks, block);
     const size_t count = (size_t)max_rows * (size_t)W * 3;  // doubles per (padded) tile
     const int b = (int)(g->k & 1);
-    const int n = (int)g->subs.size();
+    const int n = g->nlocal();
     // every part's options and buffers are checked / allocated before any work is enqueued: a failure
     // here returns before this rank joins the collective, never between its render and its gather
     std::vector<rr_render_opts> opts(n, *o);
@@ -286,7 +298,7 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
         so.nparts = g->nranks;
         so.block_rows = block;
         so.flags = RR_OUT_AVG | (o->flags & RR_NO_FRAME_TIMING);
-        int rc = render_validate(g->subs[l], cam, &so);
+        int rc = render_validate(g->subs[b][l], cam, &so);
         if (rc != RR_OK) return rc;
         GHIP(hipSetDevice(g->devices[l]));
         if (g->root_here() && l == 0)
@@ -302,11 +314,12 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
         GHIP(hipSetDevice(g->devices[l]));
         const bool root = g->root_here() && l == 0;
         void* t = root ? g->recv[b].p : g->tile[b][l].p;
-        // the gather that last read this buffer (two frames ago) must be done before it is overwritten
-        GHIP(hipStreamWaitEvent(g->render_st[l], g->ev_gathered[b][l], 0));
-        int rc = rr_render_device(g->subs[l], cam, &opts[l], nullptr, t, g->render_st[l]);
+        // the gather that last read this buffer (two frames ago) must be done before it is overwritten; the
+        // render context and stream of set b are free once that frame's render is (same stream)
+        GHIP(hipStreamWaitEvent(g->render_st[b][l], g->ev_gathered[b][l], 0));
+        int rc = rr_render_device(g->subs[b][l], cam, &opts[l], nullptr, t, g->render_st[b][l]);
         if (rc != RR_OK) return rc;
-        GHIP(hipEventRecord(g->ev_rendered[b][l], g->render_st[l]));
+        GHIP(hipEventRecord(g->ev_rendered[b][l], g->render_st[b][l]));
         GHIP(hipStreamWaitEvent(g->gather_stream(l), g->ev_rendered[b][l], 0));
     }
     if (g->virt) {
@@ -367,9 +380,9 @@ int group_render(rr_group* g, const rr_camera* cam, const rr_render_opts* o, dou
     so.flags = RR_OUT_AVG;
     int rc = group_render_gather(g, cam, &so, g->root_here() ? g->frame.p : nullptr, nullptr);
     if (rc != RR_OK) return rc;
-    for (size_t l = 0; l < g->subs.size(); ++l) {
+    for (int l = 0; l < g->nlocal(); ++l) {
         GHIP(hipSetDevice(g->devices[l]));
-        GHIP(hipStreamSynchronize(g->render_st[l]));
+        for (int b = 0; b < 2; ++b) GHIP(hipStreamSynchronize(g->render_st[b][l]));
         GHIP(hipStreamSynchronize(g->comm_st[l]));
     }
     if (g->root_here() && out_avg && (o->flags & RR_OUT_AVG)) {
@@ -389,7 +402,7 @@ int group_render(rr_group* g, const rr_camera* cam, const rr_render_opts* o, dou
 int group_last_stats(rr_group* g, rr_stats* s) {
     if (!s) return gfail(RR_E_ARG, "null stats");
     std::memset(s, 0, sizeof(*s));
-    for (rr_ctx* c : g->subs) {  // sum over this process's devices
+    for (rr_ctx* c : g->subs[g->last()]) {  // the latest frame's contexts, summed over this process's devices
         rr_stats t;
         int rc = rr_last_stats(c, &t);
         if (rc != RR_OK) return rc;
@@ -411,12 +424,34 @@ int group_last_stats(rr_group* g, rr_stats* s) {
     return RR_OK;
 }
 
-rr_ctx* group_local(rr_group* g, int l) { return (l >= 0 && l < (int)g->subs.size()) ? g->subs[l] : nullptr; }
+rr_ctx* group_local(rr_group* g, int l) { return (l >= 0 && l < g->nlocal()) ? g->subs[0][l] : nullptr; }
+
+// per-launch kernel timing on local part 0: both render contexts (their launches alternate by frame)
+int group_kernel_profile(rr_group* g, int enable) {
+    for (int b = 0; b < 2; ++b) {
+        int rc = rr_kernel_profile(g->subs[b][0], enable);
+        if (rc != RR_OK) return rc;
+    }
+    return RR_OK;
+}
+int group_kernel_times(rr_group* g, double* ms, uint64_t* launches, int32_t n) {
+    std::vector<double> m2(n > 0 ? n : 0, 0.0);
+    std::vector<uint64_t> l2(n > 0 ? n : 0, 0);
+    int rc = rr_kernel_times(g->subs[0][0], ms, launches, n);
+    if (rc < 0) return rc;
+    rc = rr_kernel_times(g->subs[1][0], m2.data(), l2.data(), n);
+    if (rc < 0) return rc;
+    for (int k = 0; k < n && k < rc; ++k) {
+        if (ms) ms[k] += m2[k];
+        if (launches) launches[k] += l2[k];
+    }
+    return rc;
+}
 
 int group_info(const rr_group* g, int32_t* nranks, int32_t* rank0, int32_t* nlocal) {
     if (nranks) *nranks = g->nranks;
     if (rank0) *rank0 = g->rank0;
-    if (nlocal) *nlocal = (int32_t)g->subs.size();
+    if (nlocal) *nlocal = (int32_t)g->nlocal();
     return RR_OK;
 }
 

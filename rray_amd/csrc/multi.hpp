@@ -11,8 +11,8 @@ struct rr_group;
 
 namespace rr {
 
-// `subs[l]` are ordinary single-device contexts created by the caller (one per local device); the
-// group takes ownership.  Global ranks rank0 .. rank0 + nlocal - 1 live in this process.
+// Per local device the group owns two ordinary single-device contexts (frames alternate between them,
+// DESIGN.md §5).  Global ranks rank0 .. rank0 + nlocal - 1 live in this process.
 int group_create_local(int n, const int* device_ids, rr_group** out);
 int group_create_rank(int device, int nranks, int rank, const uint8_t* unique_id, rr_group** out);
 // nparts virtual ranks on one device (rr_create_virtual): the same tiles, buffers, streams and
@@ -26,6 +26,9 @@ int group_render(rr_group* g, const rr_camera* cam, const rr_render_opts* o, dou
                  rr_stats* stats);
 int group_last_stats(rr_group* g, rr_stats* s);
 rr_ctx* group_local(rr_group* g, int l);  // local device context l (0 = the lowest global rank here)
+// rr_kernel_profile / rr_kernel_times for local part 0, over both of its render contexts
+int group_kernel_profile(rr_group* g, int enable);
+int group_kernel_times(rr_group* g, double* ms, uint64_t* launches, int32_t n);
 int group_info(const rr_group* g, int32_t* nranks, int32_t* rank0, int32_t* nlocal);
 // api.cpp: every argument check of rr_render_device, without enqueueing anything
 int render_validate(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o);
