@@ -80,6 +80,13 @@ struct rr_ctx {
         int32_t aa, part, nparts, block_rows;
     } tile_key{};
     bool tiles_valid = false;
+    // level-0 launch order of one-batch fused frames: every wave stores its tile's cost (clock cycles) and the
+    // tiles are re-sorted costliest-first on the first frame of a part layout and every kRR_ORDER_EVERY frames
+    DBuf tile_cost, tile_perm;
+    int64_t order_tiles = 0;  // the layout the order was built for (tiles; key below)
+    TileKey order_key{};
+    bool order_valid = false;
+    int order_age = 0;
     std::vector<DBuf> comb, comb_ext, pend;  // one per level (comb_ext: scenes with transparency)
     unsigned long long* h_counters = nullptr;
     // counters: [frame buffer 0][frame buffer 1][queries]; frames alternate (`epoch`), and each
@@ -163,6 +170,7 @@ hipError_t sync_ctx(rr_ctx* c) {
     return e;
 }
 
+constexpr int kRR_ORDER_EVERY = 64;  // frames between re-sorts of the level-0 tile order
 constexpr size_t kCounterBytes = (size_t)rr::RR_CNT_SLOTS * rr::RR_CNT_STRIDE * sizeof(unsigned long long);
 unsigned long long* frame_counters(rr_ctx* c, int k) {
     return c->counters.as<unsigned long long>() + (size_t)k * rr::RR_CNT_SLOTS * rr::RR_CNT_STRIDE;
@@ -292,6 +300,32 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
     if (P.ev_cap[0]) HIPCHK(c->ev_a.ensure(P.ev_cap[0] * sizeof(rr::Event)));
     if (P.ev_cap[1]) HIPCHK(c->ev_b.ensure(P.ev_cap[1] * sizeof(rr::Event)));
     unsigned int* lc = c->lcount.as<unsigned int>();
+    // cost-ordered level-0 tiles: one-batch fused frames of full 8x8 tiles whose level 0 is the whole frame (no
+    // secondary rays) in scenes with groups, where tile costs spread widest (mesh silhouettes against floor:
+    // C4 0.596 -> 0.511 ms per frame).  Flat scenes' tiles cost alike (C2 +0.6 % with the order), and frames
+    // with reflections lose their children queues' tile order (C3 +2 %): both keep launch order.
+    rr::LevelArgs T0 = base_args;
+    T0.base = 0;
+    set_level0_index(T0);
+    const int64_t n_tiles = T0.tile_fast ? T0.hs * T0.lrows / 64 : 0;
+    const bool order_ok = fused && c->S.has_groups && !c->S.general && (k == 0 || max_depth == 0) && B >= total && n_tiles > 0 &&
+                          n_tiles * 64 == total && n_tiles < ((int64_t)1 << 31);
+    if (order_ok) {
+        HIPCHK(c->tile_cost.ensure((size_t)n_tiles * sizeof(uint32_t)));
+        HIPCHK(c->tile_perm.ensure((size_t)n_tiles * sizeof(uint32_t)));
+        rr_ctx::TileKey key{};  // the layout only: a camera change keeps the order (costs stay a good guess)
+        key.hs = T0.hs;
+        key.lrows = T0.lrows;
+        key.aa = T0.aa;
+        key.part = T0.part;
+        key.nparts = T0.nparts;
+        key.block_rows = T0.block_rows;
+        if (c->order_tiles != n_tiles || std::memcmp(&key, &c->order_key, sizeof key) != 0) {
+            c->order_valid = false;
+            c->order_tiles = n_tiles;
+            c->order_key = key;
+        }
+    }
     for (int64_t base = 0; base < total; base += B) {
         const int64_t nb = std::min(B, total - base);
         const LevelPlan p = plan_levels(nb, k, max_depth, ext, fused);
@@ -338,9 +372,18 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             A.pending = children_possible ? c->pend[d].as<int32_t>() : nullptr;
             A.n1n2_list = c->n1n2.as<int32_t>();
             A.lcount = lc + d * rr::LC_COUNT;
+            if (order_ok && d == 0) {
+                A.tile_perm = c->order_valid ? c->tile_perm.as<uint32_t>() : nullptr;
+                A.tile_cost = c->tile_cost.as<uint32_t>();
+            }
             A.counters = frame_counters(c, c->epoch);
             A.counters_zero = (c->zero_next && d == 0 && base == 0) ? frame_counters(c, c->epoch ^ 1) : nullptr;
             HIPCHK(rr::launch_level(c->S, A, st, c->profile ? &c->prof : nullptr));
+            if (order_ok && d == 0 && (!c->order_valid || ++c->order_age >= kRR_ORDER_EVERY)) {
+                HIPCHK(rr::launch_tile_order(c->tile_cost.as<uint32_t>(), c->tile_perm.as<uint32_t>(), n_tiles, st));
+                c->order_valid = true;
+                c->order_age = 0;
+            }
         }
         // bottom-up shade_hit sums of the events with children (scene.rs:172-177); fused levels finish
         // their chains in the kernels
@@ -537,7 +580,8 @@ void rr_destroy(rr_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)sync_ctx(c);
     for (DBuf* b : {&c->culls, &c->chunks, &c->nodes, &c->groups, &c->shapes, &c->tris, &c->mats, &c->pats, &c->lights, &c->textures, &c->texels, &c->counters,
-                    &c->lcount, &c->hit, &c->n12, &c->n1n2, &c->ev_a, &c->ev_b, &c->canvas, &c->rays0, &c->qout, &c->tiles})
+                    &c->lcount, &c->hit, &c->n12, &c->n1n2, &c->ev_a, &c->ev_b, &c->canvas, &c->rays0, &c->qout, &c->tiles,
+                    &c->tile_cost, &c->tile_perm})
         b->release();
     for (auto& b : c->comb) b.release();
     for (auto& b : c->comb_ext) b.release();

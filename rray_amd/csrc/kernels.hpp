@@ -44,6 +44,11 @@ struct LevelArgs {
     void* avg;               // aa == 1: the averaged image written directly (canvas.rs:85-96 with aa = 1)
     const float* tile_bundles;  // level 0, tile_fast, affine camera: per-tile camera-ray bundles (tile_bundle_kernel,
                                 // RR_TILE_BUNDLE_FLOATS each, indexed by tile), or null: built in the walk
+    // fused level 0 of a one-batch tile_fast frame (group scenes' kernels): the tile each wave renders (launch slot -> tile, the costliest
+    // first: tile_order_kernel), or null (launch order); and where each wave stores its tile's cost in clock
+    // cycles (or null).  The order changes only which wave renders which tile, never a result.
+    const uint32_t* tile_perm;
+    uint32_t* tile_cost;
     int32_t pad_children;    // fused levels: children in per-wave 64-slot blocks (holes: Event.parent == -2)
     int32_t aa_wave;         // 2 / 4 / 8: every pixel's aa x aa samples lie in one wave's 8x8 tile and no
                              // sample has a secondary ray: the wave box-averages and writes avg (0: off)
@@ -125,6 +130,8 @@ hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t strea
 // out (n_tiles x RR_TILE_BUNDLE_FLOATS floats): exactly the bundle make_bundle's cam_tile path builds in the walk.
 constexpr int RR_TILE_BUNDLE_FLOATS = 12;
 hipError_t launch_tile_bundles(const DevScene& S, const LevelArgs& A, float* out, int64_t n_tiles, hipStream_t stream);
+// perm = tiles by decreasing recorded cost (LevelArgs.tile_cost), for the next frames' level-0 launches
+hipError_t launch_tile_order(const uint32_t* cost, uint32_t* perm, int64_t n_tiles, hipStream_t stream);
 // trace + shade run as one kernel per level (no transparent material, so no n1/n2 walk between them);
 // those levels finish their reflection chains themselves and need no combine pass
 bool fused_levels(const DevScene& S);

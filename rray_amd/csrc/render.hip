@@ -119,6 +119,41 @@ __global__ void __launch_bounds__(256) tile_bundle_kernel(LevelArgs A, float* __
     p[10] = p[11] = 0.0f;
 }
 
+// Tiles by decreasing cost (a counting sort on 256 buckets: 8 per power of two of the cycle count), so a
+// frame's costliest tiles start first and its last waves are its cheapest: the launch's tail, where CUs run
+// out of waves, shrinks.  One block; ties in a bucket land in any order (only timing depends on it).
+__global__ void __launch_bounds__(1024) tile_order_kernel(const uint32_t* __restrict__ cost, uint32_t* __restrict__ perm,
+                                                          int64_t n) {
+    __shared__ uint32_t slot[256];
+    const int t = threadIdx.x;
+    if (t < 256) slot[t] = 0;
+    __syncthreads();
+    auto bucket = [](uint32_t c) {
+        if (c == 0) return 255;
+        const int e = 31 - __clz(c);
+        const int q = e * 8 + (int)((e >= 3 ? c >> (e - 3) : c << (3 - e)) & 7u);
+        return 255 - (q > 255 ? 255 : q);
+    };
+    for (int64_t i = t; i < n; i += 1024) atomicAdd(&slot[bucket(cost[i])], 1u);
+    __syncthreads();
+    if (t == 0) {  // exclusive scan: the first slot of each bucket
+        uint32_t run = 0;
+        for (int b = 0; b < 256; ++b) {
+            const uint32_t c = slot[b];
+            slot[b] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (int64_t i = t; i < n; i += 1024) perm[atomicAdd(&slot[bucket(cost[i])], 1u)] = (uint32_t)i;
+}
+
+hipError_t launch_tile_order(const uint32_t* cost, uint32_t* perm, int64_t n_tiles, hipStream_t st) {
+    if (n_tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, cost, perm, n_tiles);
+    return hipGetLastError();
+}
+
 hipError_t launch_tile_bundles(const DevScene& S, const LevelArgs& A, float* out, int64_t n_tiles, hipStream_t st) {
     (void)S;
     if (n_tiles <= 0) return hipSuccess;
