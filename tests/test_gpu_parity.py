@@ -80,6 +80,32 @@ def test_render_matches_oracle(renderer, name, W, H, aa):
     assert got["stats"]["shade_events"] == st["shade_events"]
 
 
+def test_cost_ordered_tiles_change_no_result(R, renderer):
+    """Group scenes without secondary rays render level 0 in cost order from a layout's second frame on
+    (tile_order_kernel): frames 2..4 of the C4 thumbnail, a moved camera of the same layout
+    (the order is kept) and back, must equal the first, launch-order frame bit for bit, counters included."""
+    import math as m
+
+    scene, (o, cam) = _yaml_pair("c4_teapot.yaml", 64, 40, 2)
+    renderer.upload(scene)
+    first = renderer.render(scene.camera, aa=2, max_depth=5)
+    canvas, _ = o.render(cam, max_depth=5)
+    _compare(first["avg"], o.aa_average(canvas, 2), "c4 64x40 aa2 frame 1")
+    for k in range(3):
+        again = renderer.render(scene.camera, aa=2, max_depth=5)
+        assert np.array_equal(again["avg"], first["avg"]), f"frame {k + 2}"
+        drop = ("kernel_ms",)  # timing, not a count
+        assert {k: v for k, v in again["stats"].items() if k not in drop} == \
+            {k: v for k, v in first["stats"].items() if k not in drop}
+    t = list(scene.camera.transform)
+    moved = R.camera(128, 80, m.pi / 3.2, t)  # same layout, another view
+    mv = renderer.render(moved, aa=2, max_depth=5)
+    ref_moved = renderer.render(moved, aa=2, max_depth=5)
+    assert np.array_equal(mv["avg"], ref_moved["avg"])
+    back = renderer.render(scene.camera, aa=2, max_depth=5)
+    assert np.array_equal(back["avg"], first["avg"])
+
+
 @pytest.mark.parametrize("name,W,H,aa", [("c4_teapot.yaml", 48, 28, 2), ("c4_teapot.yaml", 40, 24, 4),
                                          ("c2_s1024.yaml", 32, 20, 4), ("c2_s1024.yaml", 16, 10, 8),
                                          ("c1_readme.yaml", 24, 16, 2)])
