@@ -120,6 +120,7 @@ def main():
     ap.add_argument("--cpu-stride", type=int, default=None,
                     help="CPU sample: one 8-row band in every STRIDE bands (default sized to ~10-30 s)")
     ap.add_argument("--no-anchor", action="store_true", help="N=1: skip the C3 scaling anchor")
+    ap.add_argument("--no-cold", action="store_true", help="N=1: skip the cold-frame measurements")
     ap.add_argument("--kernel-events", choices=("separate", "timed"), default="separate",
                     help="per-launch HIP events for the roofline: over a second pass of K steps (default) or "
                          "inside the timed region")
@@ -375,6 +376,45 @@ def cpu_leg(sess, args, gpu_img):
     return cpu, parity
 
 
+def cold_frames(R, workload, dev, local, torch):
+    """The single-shot cost the warm loop hides (the reference renders once per invocation: main.rs:73-77 ->
+    scene_builder_yaml.rs:408).  `fresh_context_ms`: a new context with the scene uploaded (untimed), its first
+    frame — workspace allocation, the per-tile camera bundles, and for group scenes the launch-order frame plus
+    the tile-order sort; `new_camera_ms`: a warm context's first frame of a moved camera (bundles recomputed);
+    `warm_ms`: the frame after it.  Host wall clock around each frame with a device synchronise."""
+    import ctypes
+
+    scene_file, W, H, aa, depth = WORKLOADS[workload]
+    text = open(os.path.join(ROOT, "scenes", scene_file)).read()
+    scene = R.YamlScene(text, W, H, aa, obj_root=scene_dir(scene_file))
+    r = R.Renderer(local)
+    r.upload(scene)
+    out = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)
+    opts = R._lib.RenderOpts(aa, depth, 0, 0, 0, 1, BLOCK, R._lib.RR_OUT_AVG | R._lib.RR_NO_FRAME_TIMING)
+    st = torch.cuda.current_stream(dev)
+
+    def frame(cam):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        r.render_device(cam, opts, None, out.data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) * 1e3
+
+    cam = scene.camera
+    first = frame(cam)
+    warm0 = frame(cam)
+    moved = type(cam)()
+    ctypes.pointer(moved)[0] = cam
+    moved.transform[3] += 1e-3  # a slightly moved camera: a new view transform, so new tile bundles
+    new_cam = frame(moved)
+    warm = frame(moved)
+    r.close()
+    return {"workload": workload, "fresh_context_ms": round(first, 4), "second_frame_ms": round(warm0, 4),
+            "new_camera_ms": round(new_cam, 4), "warm_ms": round(warm, 4),
+            "note": "host wall clock of one frame with a device synchronise on both sides (launch latency "
+                    "included): first frame of a new context, then a moved camera on the warm context"}
+
+
 def gpu_bench(args, world, mode, workload):
     import numpy as np
     import torch
@@ -399,6 +439,8 @@ def gpu_bench(args, world, mode, workload):
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import rray_amd as R
 
+    # build provenance: the library must be the build of this tree's sources (rr_build_digest)
+    lib_digest, src_digest = R._lib.check_provenance()
     dev = torch.device("cuda", local)
     torch.zeros(1, device=dev)  # torch's HIP runtime initialises first (the library shares it)
     if abi_group:
@@ -439,7 +481,9 @@ def gpu_bench(args, world, mode, workload):
             one.close()
         dist.barrier()
 
-    cpu = parity = anchor = None
+    cpu = parity = anchor = cold = None
+    if rank == 0 and world == 1 and not args.force_dist and not args.no_cold:
+        cold = [cold_frames(R, w, dev, local, torch) for w in dict.fromkeys([workload, "c4_teapot"])]
     if rank == 0 and world == 1 and not args.force_dist:
         if not args.no_cpu_baseline:
             cpu, parity = cpu_leg(sess, args, sess.frame())
@@ -466,7 +510,8 @@ def gpu_bench(args, world, mode, workload):
                            "aa": sess.aa, "max_depth": sess.depth, "samples_per_step": samples_per_frame,
                            "objects": sess.counts["objects"], "frames_per_step": frames_per_step,
                            "parallelism": par},
-                "roofline": roofline, "cpu_baseline": cpu, "parity_sample": parity,
+                "roofline": roofline, "cpu_baseline": cpu, "parity_sample": parity, "cold_frames": cold,
+                "build": {"library_digest": lib_digest, "source_digest": src_digest, "match": lib_digest == src_digest},
                 "tile_identity": identity, "scaling_anchor": anchor, "single_gpu": single,
                 "speedup_vs_single_gpu": round(value / single["value"], 3) if single else None,
                 "kernels_ms_per_step": {k: round(v[0] / steps, 4) for k, v in ktimes.items() if v[1]},

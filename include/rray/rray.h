@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 7
+#define RR_ABI_VERSION 8
 
 /* error codes */
 #define RR_OK 0
@@ -199,7 +199,12 @@ int rr_create_virtual(int device, int nparts, rr_ctx** out);
 /* ABI 7: host restatement of the root's un-interleave (the same index arithmetic as the device kernel):
  * gathered = nparts tiles back to back, each rr_part_rows(height, 0, nparts, block_rows, NULL) rows of
  * width*3 doubles (part p's rows in increasing y, padded) -> frame = height rows in frame order.  No
- * device needed (CPU rehearsals of the N > 1 path use it). */
+ * device needed (CPU rehearsals of the N > 1 path use it).  The buffers are not checked: `gathered` must
+ * hold nparts * tile_rows * width * 3 doubles and `frame` height * width * 3 (rray_amd.unshuffle checks
+ * its array's shape before the call). */
+/* ABI 8: build provenance — the sha256 prefix of the product sources this library was built from
+ * (rray_amd/build.py source_digest(): rray_amd/csrc/*, this header, the build script).  Static string. */
+const char* rr_build_digest(void);
 int rr_unshuffle_host(const double* gathered, double* frame, int64_t width, int64_t height, int32_t nparts,
                       int32_t block_rows);
 /* Whole frame -> d_frame (W*H*3 doubles on rank 0's device; ignored on other ranks), enqueued after

@@ -76,7 +76,7 @@ EXPORTS = ["rr_abi_version", "rr_last_error", "rr_device_count", "rr_create", "r
            "rr_is_shadowed", "rr_scene_inspect", "rr_scene_from_yaml", "rr_scene_desc_of", "rr_scene_free", "rr_quantize",
            "rr_write_png", "rr_render_scene_from_file", "rr_render_scene_from_file_devices", "rr_create_multi",
            "rr_rccl_unique_id", "rr_create_rank", "rr_context_info", "rr_render_gather_device", "rr_create_virtual",
-           "rr_unshuffle_host"]
+           "rr_unshuffle_host", "rr_build_digest"]
 RCCL_ID_BYTES = 128
 
 _lib = None
@@ -132,8 +132,26 @@ def lib():
     L.rr_unshuffle_host.argtypes = [_D, _D, C.c_int64, C.c_int64, C.c_int32, C.c_int32]
     L.rr_render_gather_device.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(RenderOpts), C.c_void_p,
                                           C.c_void_p]
+    L.rr_build_digest.restype = C.c_char_p
     _lib = L
     return L
+
+
+def build_digest():
+    """The source digest baked into the loaded library (rr_build_digest)."""
+    return lib().rr_build_digest().decode()
+
+
+def check_provenance():
+    """(library digest, source digest) — raises when the loaded librray_amd.so was not built from the sources of
+    this tree (a stale prebuilt library)."""
+    from . import build
+
+    have, want = build_digest(), build.source_digest()
+    if have != want:
+        raise RuntimeError(f"{LIB_PATH} was built from sources {have}, but this tree's sources are {want}: rebuild it "
+                           "(python -c 'import __graft_entry__ as g; g.build()')")
+    return have, want
 
 
 def check(rc):

@@ -164,6 +164,27 @@ def build_variant(name, defines, verbose=False, patch=None):
     return lib
 
 
+def _digest_object(verbose=False):
+    """The sources' digest baked into the library as rr_build_digest() (build provenance: smoke() and bench.py
+    compare it with source_digest() of the tree they run from, so a stale prebuilt .so cannot pass as head).
+    Regenerated whenever the digest changes; the library is relinked when this object is newer."""
+    d = source_digest()
+    src = os.path.join(OBJ, "build_digest.cpp")
+    obj = os.path.join(OBJ, "build_digest.o")
+    text = ('// generated by rray_amd/build.py: the product sources\' digest (source_digest())\n'
+            f'extern "C" const char* rr_build_digest(void) {{ return "{d}"; }}\n')
+    if not os.path.exists(src) or open(src).read() != text:
+        open(src, "w").write(text)
+    if not os.path.exists(obj) or os.path.getmtime(obj) < os.path.getmtime(src):
+        cmd = ["g++", "-O2", "-fPIC", "-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: build_digest.cpp\n{r.stderr}")
+    return obj
+
+
 def build(verbose=False, jobs=None):
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
@@ -173,6 +194,7 @@ def build(verbose=False, jobs=None):
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, dm, verbose), SOURCES))
     check_cross_lane([o + ".resources.json" for o in objs if o.endswith(".o") and os.path.exists(o + ".resources.json")])
+    objs.append(_digest_object(verbose))
     newest = max(os.path.getmtime(o) for o in objs)
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
         cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", LIB] + objs + ["-lz", "-L/opt/rocm/lib", "-lrccl", "-Wl,-soname,librray_amd.so"]

@@ -82,7 +82,7 @@ struct rr_ctx {
     bool tiles_valid = false;
     // level-0 launch order of one-batch fused frames: every wave stores its tile's cost (clock cycles) and the
     // tiles are re-sorted costliest-first on the first frame of a part layout and every kRR_ORDER_EVERY frames
-    DBuf tile_cost, tile_perm;
+    DBuf tile_cost, tile_perm, tile_hist;
     int64_t order_tiles = 0;  // the layout the order was built for (tiles; key below)
     TileKey order_key{};
     bool order_valid = false;
@@ -313,6 +313,7 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
     if (order_ok) {
         HIPCHK(c->tile_cost.ensure((size_t)n_tiles * sizeof(uint32_t)));
         HIPCHK(c->tile_perm.ensure((size_t)n_tiles * sizeof(uint32_t)));
+        HIPCHK(c->tile_hist.ensure(256 * sizeof(uint32_t)));
         rr_ctx::TileKey key{};  // the layout only: a camera change keeps the order (costs stay a good guess)
         key.hs = T0.hs;
         key.lrows = T0.lrows;
@@ -380,7 +381,8 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             A.counters_zero = (c->zero_next && d == 0 && base == 0) ? frame_counters(c, c->epoch ^ 1) : nullptr;
             HIPCHK(rr::launch_level(c->S, A, st, c->profile ? &c->prof : nullptr));
             if (order_ok && d == 0 && (!c->order_valid || ++c->order_age >= kRR_ORDER_EVERY)) {
-                HIPCHK(rr::launch_tile_order(c->tile_cost.as<uint32_t>(), c->tile_perm.as<uint32_t>(), n_tiles, st));
+                HIPCHK(rr::launch_tile_order(c->tile_cost.as<uint32_t>(), c->tile_perm.as<uint32_t>(),
+                                             c->tile_hist.as<uint32_t>(), n_tiles, st));
                 c->order_valid = true;
                 c->order_age = 0;
             }
@@ -581,7 +583,7 @@ void rr_destroy(rr_ctx* c) {
     if (c->stream) (void)sync_ctx(c);
     for (DBuf* b : {&c->culls, &c->chunks, &c->nodes, &c->groups, &c->shapes, &c->tris, &c->mats, &c->pats, &c->lights, &c->textures, &c->texels, &c->counters,
                     &c->lcount, &c->hit, &c->n12, &c->n1n2, &c->ev_a, &c->ev_b, &c->canvas, &c->rays0, &c->qout, &c->tiles,
-                    &c->tile_cost, &c->tile_perm})
+                    &c->tile_cost, &c->tile_perm, &c->tile_hist})
         b->release();
     for (auto& b : c->comb) b.release();
     for (auto& b : c->comb_ext) b.release();
@@ -620,6 +622,11 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     HIPCHK(upload(c->texels, hs.texels, st));
     HIPCHK(hipStreamSynchronize(st));
     c->host = std::move(hs);
+    // the level-0 tile order is the previous scene's tile costs: drop it (the next frame records new ones).
+    // The tile bundles depend on the camera only; they are rebuilt too, for a clean start
+    c->order_valid = false;
+    c->order_age = 0;
+    c->tiles_valid = false;
     rr::DevScene& S = c->S;
     S.culls = c->culls.as<rr::DevCull>();
     S.chunks = c->chunks.as<rr::DevChunk>();

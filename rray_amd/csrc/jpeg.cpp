@@ -47,6 +47,9 @@ bool build_huff(Huff& h, const uint8_t counts[16], const uint8_t* vals, int nval
         h.valptr[l] = k;
         h.mincode[l] = code;
         for (int i = 0; i < counts[l - 1]; ++i, ++k, ++code) {
+            // over-subscribed code (T.81 C.2): an l-bit code must stay below 2^l.  Checked before the
+            // lookahead fill, whose index code << (9 - l) would otherwise run past fast[512]
+            if (code >= (1 << l) || k >= nvals) return false;
             if (l <= 9) {
                 int lo = code << (9 - l), n = 1 << (9 - l);
                 for (int j = 0; j < n; ++j) h.fast[lo + j] = (uint16_t)((l << 8) | h.vals[k]);
@@ -408,6 +411,7 @@ struct Decoder {
     // one scan (interleaved if several components); leaves pos at the next marker after its data
     int read_scan(const uint8_t* p, int L, size_t& pos) {
         if (!frame) return fail(RR_E_IO, "JPEG scan before the frame header");
+        if (L < 1) return fail(RR_E_IO, "corrupt JPEG scan header");
         int ns = p[0];
         if (ns < 1 || ns > (int)comps.size() || L < 4 + 2 * ns) return fail(RR_E_IO, "corrupt JPEG scan header");
         ss = p[1 + 2 * ns];

@@ -130,8 +130,9 @@ hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t strea
 // out (n_tiles x RR_TILE_BUNDLE_FLOATS floats): exactly the bundle make_bundle's cam_tile path builds in the walk.
 constexpr int RR_TILE_BUNDLE_FLOATS = 12;
 hipError_t launch_tile_bundles(const DevScene& S, const LevelArgs& A, float* out, int64_t n_tiles, hipStream_t stream);
-// perm = tiles by decreasing recorded cost (LevelArgs.tile_cost), for the next frames' level-0 launches
-hipError_t launch_tile_order(const uint32_t* cost, uint32_t* perm, int64_t n_tiles, hipStream_t stream);
+// perm = tiles by decreasing recorded cost (LevelArgs.tile_cost), for the next frames' level-0 launches;
+// scratch = 256 u32 of device memory (bucket counters)
+hipError_t launch_tile_order(const uint32_t* cost, uint32_t* perm, uint32_t* scratch, int64_t n_tiles, hipStream_t stream);
 // trace + shade run as one kernel per level (no transparent material, so no n1/n2 walk between them);
 // those levels finish their reflection chains themselves and need no combine pass
 bool fused_levels(const DevScene& S);

@@ -121,36 +121,80 @@ __global__ void __launch_bounds__(256) tile_bundle_kernel(LevelArgs A, float* __
 
 // Tiles by decreasing cost (a counting sort on 256 buckets: 8 per power of two of the cycle count), so a
 // frame's costliest tiles start first and its last waves are its cheapest: the launch's tail, where CUs run
-// out of waves, shrinks.  One block; ties in a bucket land in any order (only timing depends on it).
-__global__ void __launch_bounds__(1024) tile_order_kernel(const uint32_t* __restrict__ cost, uint32_t* __restrict__ perm,
-                                                          int64_t n) {
-    __shared__ uint32_t slot[256];
-    const int t = threadIdx.x;
-    if (t < 256) slot[t] = 0;
+// out of waves, shrinks.  Ties in a bucket land in any order (only timing depends on it).  Three small
+// launches over many blocks (the one-block sort took 159 us for C4's 129 600 tiles, most of a cold frame's
+// extra cost): per-block LDS histograms added into 256 global counters, an exclusive scan of the 256, then a
+// scatter in which each block reserves its run of every bucket with one global atomic per non-empty bucket.
+__device__ __forceinline__ int cost_bucket(uint32_t c) {
+    if (c == 0) return 255;
+    const int e = 31 - __clz(c);
+    const int q = e * 8 + (int)((e >= 3 ? c >> (e - 3) : c << (3 - e)) & 7u);
+    return 255 - (q > 255 ? 255 : q);
+}
+constexpr int RR_ORDER_BLOCK = 256, RR_ORDER_PER_THREAD = 16;  // 4096 tiles per block
+__global__ void __launch_bounds__(RR_ORDER_BLOCK) tile_hist_kernel(const uint32_t* __restrict__ cost,
+                                                                   uint32_t* __restrict__ hist, int64_t n) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
     __syncthreads();
-    auto bucket = [](uint32_t c) {
-        if (c == 0) return 255;
-        const int e = 31 - __clz(c);
-        const int q = e * 8 + (int)((e >= 3 ? c >> (e - 3) : c << (3 - e)) & 7u);
-        return 255 - (q > 255 ? 255 : q);
-    };
-    for (int64_t i = t; i < n; i += 1024) atomicAdd(&slot[bucket(cost[i])], 1u);
-    __syncthreads();
-    if (t == 0) {  // exclusive scan: the first slot of each bucket
-        uint32_t run = 0;
-        for (int b = 0; b < 256; ++b) {
-            const uint32_t c = slot[b];
-            slot[b] = run;
-            run += c;
-        }
+    const int64_t b0 = (int64_t)blockIdx.x * RR_ORDER_BLOCK * RR_ORDER_PER_THREAD;
+    for (int k = 0; k < RR_ORDER_PER_THREAD; ++k) {
+        const int64_t i = b0 + (int64_t)k * RR_ORDER_BLOCK + threadIdx.x;
+        if (i < n) atomicAdd(&h[cost_bucket(cost[i])], 1u);
     }
     __syncthreads();
-    for (int64_t i = t; i < n; i += 1024) perm[atomicAdd(&slot[bucket(cost[i])], 1u)] = (uint32_t)i;
+    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+// hist -> exclusive prefix (the first slot of each bucket), in place; one block of 256
+__global__ void __launch_bounds__(256) tile_scan_kernel(uint32_t* __restrict__ hist) {
+    __shared__ uint32_t v[256];
+    const int t = threadIdx.x;
+    v[t] = hist[t];
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {  // Hillis-Steele inclusive scan
+        const uint32_t a = t >= off ? v[t - off] : 0u;
+        __syncthreads();
+        v[t] += a;
+        __syncthreads();
+    }
+    hist[t] = t ? v[t - 1] : 0u;
+}
+__global__ void __launch_bounds__(RR_ORDER_BLOCK) tile_scatter_kernel(const uint32_t* __restrict__ cost,
+                                                                      uint32_t* __restrict__ cursor,
+                                                                      uint32_t* __restrict__ perm, int64_t n) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t b0 = (int64_t)blockIdx.x * RR_ORDER_BLOCK * RR_ORDER_PER_THREAD;
+    int bk[RR_ORDER_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < RR_ORDER_PER_THREAD; ++k) {
+        const int64_t i = b0 + (int64_t)k * RR_ORDER_BLOCK + threadIdx.x;
+        bk[k] = i < n ? cost_bucket(cost[i]) : -1;
+        if (bk[k] >= 0) atomicAdd(&h[bk[k]], 1u);
+    }
+    __syncthreads();
+    // this block's run of each bucket: one global atomic per non-empty bucket
+    const uint32_t c = h[threadIdx.x];
+    __syncthreads();
+    h[threadIdx.x] = c ? atomicAdd(&cursor[threadIdx.x], c) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < RR_ORDER_PER_THREAD; ++k) {
+        const int64_t i = b0 + (int64_t)k * RR_ORDER_BLOCK + threadIdx.x;
+        if (bk[k] >= 0) perm[atomicAdd(&h[bk[k]], 1u)] = (uint32_t)i;
+    }
 }
 
-hipError_t launch_tile_order(const uint32_t* cost, uint32_t* perm, int64_t n_tiles, hipStream_t st) {
+// scratch: 256 u32 of device memory for the bucket counters
+hipError_t launch_tile_order(const uint32_t* cost, uint32_t* perm, uint32_t* scratch, int64_t n_tiles, hipStream_t st) {
     if (n_tiles <= 0) return hipSuccess;
-    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, cost, perm, n_tiles);
+    const unsigned blocks = (unsigned)((n_tiles + RR_ORDER_BLOCK * RR_ORDER_PER_THREAD - 1) / (RR_ORDER_BLOCK * RR_ORDER_PER_THREAD));
+    hipError_t e = hipMemsetAsync(scratch, 0, 256 * sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(tile_hist_kernel, dim3(blocks), dim3(RR_ORDER_BLOCK), 0, st, cost, scratch, n_tiles);
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(256), 0, st, scratch);
+    hipLaunchKernelGGL(tile_scatter_kernel, dim3(blocks), dim3(RR_ORDER_BLOCK), 0, st, cost, scratch, perm, n_tiles);
     return hipGetLastError();
 }
 

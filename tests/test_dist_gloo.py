@@ -141,3 +141,20 @@ def test_host_unshuffle_matches_partition():
             assert len(pr) <= rows
             gathered[p * rows: p * rows + len(pr)] = frame[pr]
         assert np.array_equal(R.unshuffle(gathered, H, world, block), frame), (H, world, block)
+
+
+def test_host_unshuffle_refuses_wrong_shapes():
+    """rr_unshuffle_host reads nparts * tile_rows rows of W * 3 doubles: rray_amd.unshuffle refuses a buffer
+    of any other shape (a short tile, a 4-channel tile, a 2-D array) before the library can read past it."""
+    import rray_amd as R
+
+    H, world, block, W = 40, 3, 8, 5
+    rows = len(R.part_rows(H, 0, world, block))
+    ok = np.zeros((world * rows, W, 3))
+    assert R.unshuffle(ok, H, world, block).shape == (H, W, 3)
+    for bad in (np.zeros((world * rows - 1, W, 3)), np.zeros((world * rows, W, 4)), np.zeros((world * rows, W * 3)),
+                np.zeros((world * (rows + 1), W, 3))):
+        with pytest.raises(ValueError):
+            R.unshuffle(bad, H, world, block)
+    with pytest.raises(ValueError):
+        R.unshuffle(ok, H, 0, block)

@@ -134,3 +134,70 @@ def test_jpeg_outside_the_decoder_is_refused(R, tmp_path):
     with pytest.raises(R.RRError) as e:
         texels(R, str(q))
     assert e.value.code == -6
+
+
+def _with_segment_before_sos(data: bytes, seg: bytes) -> bytes:
+    at = data.index(b"\xff\xda")
+    return data[:at] + seg + data[at:]
+
+
+@pytest.mark.parametrize("counts", [[3] + [0] * 15, [2, 3] + [0] * 14, [0] * 6 + [127, 3] + [0] * 8])
+def test_oversubscribed_huffman_table_is_refused(R, tmp_path, counts):
+    """A DHT whose codes do not fit their lengths (T.81 C.2: an l-bit code must stay below 2^l) is a
+    corrupt file (RR_E_IO), refused before its lookahead-table write (each of these would index the 9-bit
+    lookahead at 512 or beyond: an extra 1-bit, 2-bit or 8-bit code)."""
+    p = str(tmp_path / "t.jpg")
+    PIL.fromarray(smooth(16, 16)).save(p, quality=90)
+    body = bytes([0x00]) + bytes(counts) + bytes(range(sum(counts)))
+    seg = b"\xff\xc4" + (len(body) + 2).to_bytes(2, "big") + body
+    q = tmp_path / "bad.jpg"
+    q.write_bytes(_with_segment_before_sos(open(p, "rb").read(), seg))
+    with pytest.raises(R.RRError) as e:
+        texels(R, str(q))
+    assert e.value.code == -6
+
+
+def test_empty_scan_header_is_refused(R, tmp_path):
+    """An SOS segment of length 2 (no component count) at the end of the file: RR_E_IO, no read past it."""
+    p = str(tmp_path / "t.jpg")
+    PIL.fromarray(smooth(16, 16)).save(p, quality=90)
+    data = open(p, "rb").read()
+    q = tmp_path / "sos.jpg"
+    q.write_bytes(data[:data.index(b"\xff\xda")] + b"\xff\xda\x00\x02")
+    with pytest.raises(R.RRError) as e:
+        texels(R, str(q))
+    assert e.value.code == -6
+
+
+def test_corrupt_jpegs_under_asan(tmp_path):
+    """The decoder itself (jpeg.cpp, host code) built with g++ -fsanitize=address on the corrupt files
+    above: every one is refused (RR_E_IO) with no out-of-bounds access reported."""
+    import shutil
+    import subprocess
+
+    if not shutil.which("g++"):
+        pytest.skip("no g++")
+    exe = str(tmp_path / "jpeg_asan")
+    r = subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address", "-fno-omit-frame-pointer",
+                        "-I" + os.path.join(ROOT, "include"), os.path.join(ROOT, "tools", "asan_jpeg_main.cpp"),
+                        os.path.join(ROOT, "rray_amd", "csrc", "jpeg.cpp"), "-o", exe], capture_output=True, text=True)
+    if r.returncode != 0 and "sanitize" in r.stderr:
+        pytest.skip("AddressSanitizer unavailable")
+    assert r.returncode == 0, r.stderr
+    p = str(tmp_path / "t.jpg")
+    PIL.fromarray(smooth(16, 16)).save(p, quality=90)
+    data = open(p, "rb").read()
+    files = []
+    for i, counts in enumerate([[3] + [0] * 15, [2, 3] + [0] * 14, [0] * 6 + [127, 3] + [0] * 8]):
+        body = bytes([0x00]) + bytes(counts) + bytes(range(sum(counts)))
+        f = tmp_path / f"dht{i}.jpg"
+        f.write_bytes(_with_segment_before_sos(data, b"\xff\xc4" + (len(body) + 2).to_bytes(2, "big") + body))
+        files.append(str(f))
+    f = tmp_path / "sos.jpg"
+    f.write_bytes(data[:data.index(b"\xff\xda")] + b"\xff\xda\x00\x02")
+    files.append(str(f))
+    r = subprocess.run([exe, p] + files, capture_output=True, text=True,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    rcs = [int(line.split()[0]) for line in r.stdout.splitlines()]
+    assert rcs == [0] + [-6] * len(files), r.stdout
