@@ -26,7 +26,11 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "
           "-I" + os.path.join(ROOT, "include")]
 DEVICE = ["--offload-arch=" + ARCH, "-mllvm", "-disable-promote-alloca-to-lds"]
 LEVEL_UNITS = [f"render_levels_g{g}_{lc}.hip" for g in (2, 1, 0) for lc in ("lds", "gl")]  # slowest first
-SOURCES = LEVEL_UNITS + ["render.hip", "api.cpp", "multi.cpp", "flatten.cpp", "frontend.cpp", "yaml.cpp", "png.cpp", "jpeg.cpp"]
+CHAIN_UNITS = [f"render_chain_g{g}_{lc}.hip" for g in (2, 1, 0) for lc in ("lds", "gl")]
+# per-unit flags: the chain kernels' loop must not get loop-invariant constants hoisted into registers (they
+# spill instead of being rematerialised)
+UNIT_FLAGS = {u: ["-mllvm", "-disable-machine-licm"] for u in CHAIN_UNITS}
+SOURCES = LEVEL_UNITS + CHAIN_UNITS + ["render.hip", "api.cpp", "multi.cpp", "flatten.cpp", "frontend.cpp", "yaml.cpp", "png.cpp", "jpeg.cpp"]
 
 
 def source_digest():
@@ -71,11 +75,13 @@ def _resources(stderr):
 
 def cross_lane_kernel(demangled):
     """device_core.inc cross_lane_ok: kernels whose walks read other lanes' registers (v_readlane)."""
-    m = re.search(r"rr::(shade_kernel|trace_kernel|n1n2_kernel|shadow_query_kernel)<([^>]*)>", demangled)
+    m = re.search(r"rr::(shade_kernel|trace_kernel|n1n2_kernel|shadow_query_kernel|chain_kernel)<([^>]*)>", demangled)
     if not m:
         return False
     args = [a.strip() for a in m.group(2).split(",")]
     g = int(args[0])
+    if m.group(1) == "chain_kernel":  # <G, LC, PRE, CP, AR, RM>: XL in the flat scenes' kernels only
+        return g == 0 and args[3] == "false" and args[4] == "false"
     if m.group(1) == "shade_kernel":  # <G, LC, FUSED, PRE, CP, RM, AR>
         return g < 2 and args[4] == "false" and args[6] == "false"
     return g < 2
@@ -105,7 +111,7 @@ def _compile(src, deps_mtime, verbose):
     path = os.path.join(CSRC, src)
     if os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(path), deps_mtime):
         return out
-    cmd = [HIPCC] + COMMON + DEVICE + ["-c", path, "-o", out]
+    cmd = [HIPCC] + COMMON + DEVICE + UNIT_FLAGS.get(src, []) + ["-c", path, "-o", out]
     if src.endswith(".cpp"):
         cmd = [HIPCC, "-x", "hip"] + COMMON + DEVICE + ["-c", path, "-o", out]
     else:
@@ -146,7 +152,7 @@ def build_variant(name, defines, verbose=False, patch=None):
         o = os.path.join(out_dir, os.path.splitext(src)[0] + ".o")
         pre = [HIPCC, "-x", "hip"] if src.endswith(".cpp") else [HIPCC]
         inc = ["-I" + os.path.join(os.path.dirname(os.path.dirname(csrc)), "include")] if patch else []
-        cmd = pre + COMMON + inc + DEVICE + flags + ["-c", os.path.join(csrc, src), "-o", o]
+        cmd = pre + COMMON + inc + DEVICE + UNIT_FLAGS.get(src, []) + flags + ["-c", os.path.join(csrc, src), "-o", o]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

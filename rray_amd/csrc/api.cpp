@@ -263,35 +263,42 @@ int tile_bundles(rr_ctx* c, const rr::LevelArgs& base_args, hipStream_t st, cons
 // pixel's samples lie in one wave's 8x8 tile (aa in {2, 4, 8}, full tiles: the tile_fast layout) and no
 // sample spawns a secondary ray (fused levels with no reflective / transparent material, or depth 0).
 bool wave_avg_ok(const rr_ctx* c, int32_t aa, int64_t hs, int64_t local_rows, int max_depth) {
+    // (reflection chains run inside the level-0 wave, chain_levels: every sample is final in its wave too)
     return (aa == 2 || aa == 4 || aa == 8) && hs % 8 == 0 && local_rows % 8 == 0 && local_rows > 0 &&
-           rr::fused_levels(c->S) && (c->host.max_children == 0 || max_depth == 0);
+           rr::fused_levels(c->S) &&
+           (c->host.max_children == 0 || max_depth == 0 || rr::chain_levels(c->S, c->host.max_children, max_depth));
 }
 
 int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max_depth, double* out, hipStream_t st,
                void* avg = nullptr, int32_t avg_f32 = 0, int32_t aa_wave = 0) {
-    const int k = c->host.max_children;
     const bool ext = c->host.has_transparent != 0;
     const bool fused = rr::fused_levels(c->S);
+    // reflection chains inside the level-0 waves (chain_kernel): one level, no recursion queues
+    const bool chain = rr::chain_levels(c->S, c->host.max_children, max_depth);
+    const int k = chain ? 0 : c->host.max_children;
+    const int plan_depth = chain ? 0 : max_depth;
     // batch: at most c->batch camera samples, shrunk (power-of-two steps, tile-aligned) until the
     // worst-case queues fit the context's budget and every event index fits in int32
     int64_t B = std::max<int64_t>(64, std::min<int64_t>(c->batch, total));
     for (;;) {
-        const LevelPlan p = plan_levels(B, k, max_depth, ext, fused);
+        const LevelPlan p = plan_levels(B, k, plan_depth, ext, fused);
         const int64_t last = p.cap[p.levels - 1];
         if (B <= 4096 || (p.bytes <= c->queue_budget && last < ((int64_t)1 << 31) && p.max_cap < ((int64_t)1 << 31)))
             break;
         B = std::max<int64_t>(4096, (B / 2) & ~(int64_t)63);
     }
-    const LevelPlan P = plan_levels(B, k, max_depth, ext, fused);
+    const LevelPlan P = plan_levels(B, k, plan_depth, ext, fused);
     if (P.max_cap >= ((int64_t)1 << 31)) return fail(RR_E_LIMIT, "recursion queues exceed 2^31 events (lower max_depth)");
     if ((int)c->comb.size() < P.levels) {
         c->comb.resize(P.levels);
         c->comb_ext.resize(P.levels);
         c->pend.resize(P.levels);
     }
-    HIPCHK(c->hit.ensure(P.max_cap * sizeof(rr::HitRec)));
-    HIPCHK(c->n12.ensure(P.max_cap * 2 * sizeof(double)));
-    HIPCHK(c->n1n2.ensure(P.max_cap * sizeof(int32_t)));
+    if (!fused) {  // hit records and n1/n2 lists: the unfused trace / n1n2 / shade kernels only
+        HIPCHK(c->hit.ensure(P.max_cap * sizeof(rr::HitRec)));
+        HIPCHK(c->n12.ensure(P.max_cap * 2 * sizeof(double)));
+        HIPCHK(c->n1n2.ensure(P.max_cap * sizeof(int32_t)));
+    }
     for (int d = 0; d + 1 < P.levels; ++d) {
         HIPCHK(c->comb[d].ensure(P.cap[d] * sizeof(rr::CombRec)));
         if (ext) HIPCHK(c->comb_ext[d].ensure(P.cap[d] * sizeof(rr::CombExt)));
@@ -308,7 +315,7 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
     T0.base = 0;
     set_level0_index(T0);
     const int64_t n_tiles = T0.tile_fast ? T0.hs * T0.lrows / 64 : 0;
-    const bool order_ok = fused && c->S.has_groups && !c->S.general && (k == 0 || max_depth == 0) && B >= total && n_tiles > 0 &&
+    const bool order_ok = fused && !chain && c->S.has_groups && !c->S.general && (k == 0 || max_depth == 0) && B >= total && n_tiles > 0 &&
                           n_tiles * 64 == total && n_tiles < ((int64_t)1 << 31);
     if (order_ok) {
         HIPCHK(c->tile_cost.ensure((size_t)n_tiles * sizeof(uint32_t)));
@@ -329,7 +336,7 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
     }
     for (int64_t base = 0; base < total; base += B) {
         const int64_t nb = std::min(B, total - base);
-        const LevelPlan p = plan_levels(nb, k, max_depth, ext, fused);
+        const LevelPlan p = plan_levels(nb, k, plan_depth, ext, fused);
         // per-level queue counters [level][LC_*], zeroed once per batch (appends, pending, n1/n2 lists)
         if (p.levels > 1 || ext)
             HIPCHK(hipMemsetAsync(lc, 0, (size_t)p.levels * rr::LC_COUNT * sizeof(unsigned int), st));
@@ -379,7 +386,10 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             }
             A.counters = frame_counters(c, c->epoch);
             A.counters_zero = (c->zero_next && d == 0 && base == 0) ? frame_counters(c, c->epoch ^ 1) : nullptr;
-            HIPCHK(rr::launch_level(c->S, A, st, c->profile ? &c->prof : nullptr));
+            if (chain)
+                HIPCHK(rr::launch_chain(c->S, A, st, c->profile ? &c->prof : nullptr));
+            else
+                HIPCHK(rr::launch_level(c->S, A, st, c->profile ? &c->prof : nullptr));
             if (order_ok && d == 0 && (!c->order_valid || ++c->order_age >= kRR_ORDER_EVERY)) {
                 HIPCHK(rr::launch_tile_order(c->tile_cost.as<uint32_t>(), c->tile_perm.as<uint32_t>(),
                                              c->tile_hist.as<uint32_t>(), n_tiles, st));

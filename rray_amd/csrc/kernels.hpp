@@ -84,6 +84,7 @@ struct CombArgs {
 // stage (scenes with an area light).
 constexpr int RR_PRELIT_LIGHTS = 2;
 constexpr size_t RR_AREA_STAGE_BYTES = 3 * 256 * 8 + 2 * 256 * 4;
+constexpr size_t RR_CHAIN_STAGE_BYTES = 10 * 256 * 8;  // chain kernels: parked reflected ray + level-0 record
 
 // Level-0 camera events run in 8x8-sample tiles of the part-local supersampled canvas (8-row bands,
 // 8-column tiles inside a band; the last band / column may be narrower) so that a wave's 64 rays
@@ -117,7 +118,7 @@ __host__ __device__ inline uint32_t tile_to_local_u32(uint32_t t, uint32_t hs, u
 
 // Optional per-kernel timing: when `prof` is non-null every launch is bracketed by HIP events on
 // the launch stream and appended to it (resolved on the host after a synchronise).
-enum KernelId { K_TRACE = 0, K_N1N2, K_SHADE, K_SHADOW, K_FINISH, K_COMBINE, K_AA, K_TRACE_SHADE, K_COUNT };
+enum KernelId { K_TRACE = 0, K_N1N2, K_SHADE, K_SHADOW, K_FINISH, K_COMBINE, K_AA, K_TRACE_SHADE, K_CHAIN, K_COUNT };
 struct KernelProf {
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> marks;
     std::vector<hipEvent_t> pool;
@@ -141,6 +142,12 @@ bool fused_levels(const DevScene& S);
 template <int G, bool LC>
 void launch_level_t(const DevScene& S, const LevelArgs& A, hipStream_t stream, KernelProf* prof);
 hipError_t launch_combine(const CombArgs& C, hipStream_t stream, KernelProf* prof = nullptr);
+// Fused scenes whose materials reflect: the whole reflection chain of every level-0 event inside its wave
+// (render_levels.inc chain_kernel), one launch per batch with no recursion queues
+bool chain_levels(const DevScene& S, int max_children, int max_depth);
+template <int G, bool LC>
+void launch_chain_t(const DevScene& S, const LevelArgs& A, hipStream_t stream, KernelProf* prof);
+hipError_t launch_chain(const DevScene& S, const LevelArgs& A, hipStream_t stream, KernelProf* prof = nullptr);
 hipError_t launch_aa(const double* canvas, double* out, int64_t width, int64_t rows, int32_t aa, hipStream_t stream,
                      KernelProf* prof = nullptr);
 hipError_t launch_aa_f32(const double* canvas, float* out, int64_t width, int64_t rows, int32_t aa, hipStream_t stream,

@@ -1,0 +1,15 @@
+// render_chain_g2_gl.hip — reflection-chain kernels (render_levels.inc chain_kernel) for G = 2 (general scenes (CSG, 4-entry leaves)),
+// culls read from global memory.  A translation unit of their own: build.py compiles these without machine LICM, which otherwise
+// hoists constant materialisations (OCML pow's coefficients) out of the chain loop and spills them.
+#include <cstdlib>
+
+#include "device_core.inc"
+#include "kernels.hpp"
+#include "wavefront.hpp"
+
+namespace rr {
+#include "render_common.inc"
+#include "render_levels.inc"
+
+template void launch_chain_t<2, false>(const DevScene&, const LevelArgs&, hipStream_t, KernelProf*);
+}  // namespace rr
