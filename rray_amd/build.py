@@ -80,7 +80,7 @@ def cross_lane_kernel(demangled):
         return False
     args = [a.strip() for a in m.group(2).split(",")]
     g = int(args[0])
-    if m.group(1) == "chain_kernel":  # <G, LC, PRE, CP, AR, RM>: XL in the flat scenes' kernels only
+    if m.group(1) == "chain_kernel":  # <G, LC, PRE, CP, AR, RM0, RMD>: XL in the flat scenes' kernels only
         return g == 0 and args[3] == "false" and args[4] == "false"
     if m.group(1) == "shade_kernel":  # <G, LC, FUSED, PRE, CP, RM, AR>
         return g < 2 and args[4] == "false" and args[6] == "false"
@@ -162,6 +162,7 @@ def build_variant(name, defines, verbose=False, patch=None):
 
     with cf.ThreadPoolExecutor(min(len(SOURCES), max(1, min(16, os.cpu_count() or 1)))) as ex:
         objs = list(ex.map(one, SOURCES))
+    objs.append(_digest_object(verbose, out_dir, "variant-" + name))  # never equal to a source digest
     lib = os.path.join(out_dir, "librray_amd.so")
     r = subprocess.run([HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", lib] + objs +
                        ["-lz", "-L/opt/rocm/lib", "-lrccl", "-Wl,-soname,librray_amd.so"], capture_output=True, text=True)
@@ -170,13 +171,14 @@ def build_variant(name, defines, verbose=False, patch=None):
     return lib
 
 
-def _digest_object(verbose=False):
+def _digest_object(verbose=False, out_dir=None, digest=None):
     """The sources' digest baked into the library as rr_build_digest() (build provenance: smoke() and bench.py
     compare it with source_digest() of the tree they run from, so a stale prebuilt .so cannot pass as head).
     Regenerated whenever the digest changes; the library is relinked when this object is newer."""
-    d = source_digest()
-    src = os.path.join(OBJ, "build_digest.cpp")
-    obj = os.path.join(OBJ, "build_digest.o")
+    d = digest or source_digest()
+    out_dir = out_dir or OBJ
+    src = os.path.join(out_dir, "build_digest.cpp")
+    obj = os.path.join(out_dir, "build_digest.o")
     text = ('// generated by rray_amd/build.py: the product sources\' digest (source_digest())\n'
             f'extern "C" const char* rr_build_digest(void) {{ return "{d}"; }}\n')
     if not os.path.exists(src) or open(src).read() != text:

@@ -97,6 +97,10 @@ struct rr_ctx {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipEvent_t ev_in = nullptr, ev_out = nullptr;
     hipStream_t last_st = nullptr;  // stream of the last render (the context's workspace is ordered on it)
+    // canvas-path frames: the per-pass box averages run on aa_stream (run_levels AaPasses)
+    hipStream_t aa_stream = nullptr;
+    std::vector<hipEvent_t> pass_ev;
+    hipEvent_t aa_done = nullptr;
     rr_stats last{};
     bool stats_pending = false;
     bool frame_timed = true;  // e0/e1 bracket the last frame
@@ -269,8 +273,18 @@ bool wave_avg_ok(const rr_ctx* c, int32_t aa, int64_t hs, int64_t local_rows, in
            (c->host.max_children == 0 || max_depth == 0 || rr::chain_levels(c->S, c->host.max_children, max_depth));
 }
 
+// The box average of a canvas-path frame (aa outside the in-wave cases, e.g. C3's aa = 3) overlapped with the
+// render: the frame runs in passes of whole output rows, and each pass's rows are averaged on the context's
+// second stream while the next pass renders (the render is VALU-bound, the average HBM-bound).  Null: no passes.
+struct AaPasses {
+    void* avg;
+    int32_t f32;
+    int64_t width;  // output pixels per row
+    int32_t aa;
+};
+
 int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max_depth, double* out, hipStream_t st,
-               void* avg = nullptr, int32_t avg_f32 = 0, int32_t aa_wave = 0) {
+               void* avg = nullptr, int32_t avg_f32 = 0, int32_t aa_wave = 0, const AaPasses* aap = nullptr) {
     const bool ext = c->host.has_transparent != 0;
     const bool fused = rr::fused_levels(c->S);
     // reflection chains inside the level-0 waves (chain_kernel): one level, no recursion queues
@@ -286,6 +300,22 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
         if (B <= 4096 || (p.bytes <= c->queue_budget && last < ((int64_t)1 << 31) && p.max_cap < ((int64_t)1 << 31)))
             break;
         B = std::max<int64_t>(4096, (B / 2) & ~(int64_t)63);
+    }
+    // AA passes: batches of whole output rows (a multiple of lcm(8, aa) sample rows, so every batch is whole
+    // 8-row tile bands and whole pixels), about kRR_AA_PASSES of them
+    bool passes = false;
+    if (aap && out && !base_args.rays0 && base_args.hs % 8 == 0 && base_args.lrows % 8 == 0) {
+        int64_t rows_unit = 8;
+        while (rows_unit % aap->aa) rows_unit += 8;
+        const int64_t unit = rows_unit * base_args.hs;
+        const int64_t units = total / unit;
+        const int np = std::max(1, std::atoi(std::getenv("RRAY_AA_PASSES") ? std::getenv("RRAY_AA_PASSES") : "4"));
+        if (total % unit == 0 && units >= 2 && np > 1 && B >= unit) {
+            const int64_t per = std::min((units + np - 1) / np, B / unit);
+            B = per * unit;
+            passes = true;
+            if (!c->aa_stream) HIPCHK(hipStreamCreateWithFlags(&c->aa_stream, hipStreamNonBlocking));
+        }
     }
     const LevelPlan P = plan_levels(B, k, plan_depth, ext, fused);
     if (P.max_cap >= ((int64_t)1 << 31)) return fail(RR_E_LIMIT, "recursion queues exceed 2^31 events (lower max_depth)");
@@ -417,6 +447,36 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             C.lrows = base_args.rays0 ? 0 : base_args.lrows;
             HIPCHK(rr::launch_combine(C, st, c->profile ? &c->prof : nullptr));
         }
+        if (passes) {  // this batch's output rows, averaged on the second stream after the batch
+            const int64_t y0 = base / base_args.hs / aap->aa, y1 = (base + nb) / base_args.hs / aap->aa;
+            const size_t pi = (size_t)(base / B);
+            while (c->pass_ev.size() <= pi) {
+                hipEvent_t e = nullptr;
+                HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                c->pass_ev.push_back(e);
+            }
+            HIPCHK(hipEventRecord(c->pass_ev[pi], st));
+            HIPCHK(hipStreamWaitEvent(c->aa_stream, c->pass_ev[pi], 0));
+            const double* src = out + 3 * y0 * aap->aa * base_args.hs;
+            if (aap->f32)
+                HIPCHK(rr::launch_aa_f32(src, static_cast<float*>(aap->avg) + 3 * y0 * aap->width, aap->width, y1 - y0,
+                                         aap->aa, c->aa_stream, c->profile ? &c->prof : nullptr));
+            else
+                HIPCHK(rr::launch_aa(src, static_cast<double*>(aap->avg) + 3 * y0 * aap->width, aap->width, y1 - y0,
+                                     aap->aa, c->aa_stream, c->profile ? &c->prof : nullptr));
+        }
+    }
+    if (passes) {  // the caller's stream continues after the last pass's average
+        HIPCHK(hipEventRecord(c->aa_done, c->aa_stream));
+        HIPCHK(hipStreamWaitEvent(st, c->aa_done, 0));
+    } else if (aap) {  // one pass: the average follows on the caller's stream
+        const int64_t rows = total / base_args.hs / aap->aa;
+        if (aap->f32)
+            HIPCHK(rr::launch_aa_f32(out, static_cast<float*>(aap->avg), aap->width, rows, aap->aa, st,
+                                     c->profile ? &c->prof : nullptr));
+        else
+            HIPCHK(rr::launch_aa(out, static_cast<double*>(aap->avg), aap->width, rows, aap->aa, st,
+                                 c->profile ? &c->prof : nullptr));
     }
     return RR_OK;
 }
@@ -533,6 +593,7 @@ int rr_create(int device, rr_ctx** out) {
     if (e == hipSuccess) e = hipEventCreate(&c->e1);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->aa_done, hipEventDisableTiming);
     if (e == hipSuccess)
         e = hipHostMalloc((void**)&c->h_counters, kCounterBytes, hipHostMallocDefault);
     if (e == hipSuccess) e = c->counters.ensure(3 * kCounterBytes);
@@ -604,6 +665,9 @@ void rr_destroy(rr_ctx* c) {
     if (c->e1) (void)hipEventDestroy(c->e1);
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     if (c->ev_out) (void)hipEventDestroy(c->ev_out);
+    if (c->aa_done) (void)hipEventDestroy(c->aa_done);
+    for (hipEvent_t e : c->pass_ev) (void)hipEventDestroy(e);
+    if (c->aa_stream) (void)hipStreamDestroy(c->aa_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -838,17 +902,13 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     rc = tile_bundles(c, A, st, &A.tile_bundles);
     if (rc != RR_OK) return rc;
     c->zero_next = true;
-    rc = run_levels(c, A, total, o->max_depth, canvas, st, direct_avg ? d_avg : nullptr, f32, wave_avg ? o->aa : 0);
+    const AaPasses aap{d_avg, f32, W, o->aa};
+    rc = run_levels(c, A, total, o->max_depth, canvas, st, direct_avg ? d_avg : nullptr, f32, wave_avg ? o->aa : 0,
+                    (d_avg && !direct_avg) ? &aap : nullptr);
     c->zero_next = false;
     if (rc != RR_OK) return rc;
     c->stats_src = frame_counters(c, c->epoch);
     c->epoch ^= 1;
-    if (d_avg && !direct_avg && f32)
-        HIPCHK(rr::launch_aa_f32(canvas, static_cast<float*>(d_avg), W, rows, o->aa, st,
-                                 c->profile ? &c->prof : nullptr));
-    else if (d_avg && !direct_avg)
-        HIPCHK(rr::launch_aa(canvas, static_cast<double*>(d_avg), W, rows, o->aa, st,
-                             c->profile ? &c->prof : nullptr));
     if (c->frame_timed) HIPCHK(hipEventRecord(c->e1, st));
     c->stats_pending = true;
     // C_SAMPLES is not incremented by the wavefront kernels; it is the level-0 event count
