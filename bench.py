@@ -53,6 +53,7 @@ def scene_dir(scene_file):
 SINGLE_GPU_WORKLOAD = "c2_s1024"      # BASELINE configs[1]
 MULTI_GPU_WORKLOAD = "c3_s1024_reflect"  # BASELINE configs[2]
 BLOCK = 8  # output rows per interleaved block
+DEPTH_OVERRIDE = None  # --max-depth (experiments only)
 # SURVEY.md §8(d) algorithmic flop model (FMA = 2, sqrt/div = 1): per leaf test and per shade event
 FLOPS = {"sphere": 57, "plane": 13, "tri": 45, "group": 45, "shade": 250}
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (256 CU x 2.4 GHz x 128 flop/clk), MI355X_MICROARCH.md
@@ -121,6 +122,8 @@ def main():
                     help="CPU sample: one 8-row band in every STRIDE bands (default sized to ~10-30 s)")
     ap.add_argument("--no-anchor", action="store_true", help="N=1: skip the C3 scaling anchor")
     ap.add_argument("--no-cold", action="store_true", help="N=1: skip the cold-frame measurements")
+    ap.add_argument("--max-depth", type=int, default=None,
+                    help="experiment: override the workload's recursion depth (the line then names it in config)")
     ap.add_argument("--kernel-events", choices=("separate", "timed"), default="separate",
                     help="per-launch HIP events for the roofline: over a second pass of K steps (default) or "
                          "inside the timed region")
@@ -133,6 +136,8 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank path: gloo, oracle-rendered thumbnail tiles, no GPU")
     args = ap.parse_args()
+    global DEPTH_OVERRIDE
+    DEPTH_OVERRIDE = args.max_depth
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args))
@@ -156,6 +161,8 @@ class Session:
 
         self.workload = workload
         self.scene_file, self.W, self.H, self.aa, self.depth = WORKLOADS[workload]
+        if DEPTH_OVERRIDE is not None:
+            self.depth = DEPTH_OVERRIDE
         self.text = open(os.path.join(ROOT, "scenes", self.scene_file)).read()
         self.scene = R.YamlScene(self.text, self.W, self.H, self.aa, obj_root=scene_dir(self.scene_file))
         self.counts = scene_counts(self.scene.desc())
@@ -268,11 +275,16 @@ def roofline_of(sess, ktimes, stats, steps, in_region):
         ktimes = {"none": (0.0, 1)}
     dom = max(ktimes, key=lambda k: ktimes[k][0])
     dom_ms, dom_n = ktimes[dom]
+    if dom in ("chain", "deep"):  # the chain kernels' two launches share one flop count (every walk of the frame)
+        dom = "chain"
+        dom_ms = sum(ktimes[k][0] for k in ("chain", "deep") if k in ktimes)
+        dom_n = ktimes["chain"][1] if "chain" in ktimes else dom_n
     # f64 flops this kernel executed in the last step: the exact leaf tests its walks ran after culling
     # (trace / n1n2 walks; the shade kernel runs the is_shadowed walks) + the shade-event model
     ef = stats["exact_flops"]
     flops = {"trace": ef[0], "n1n2": ef[2], "shade": ef[1] + stats["shade_events"] * FLOPS["shade"],
-             "trace_shade": ef[0] + ef[1] + stats["shade_events"] * FLOPS["shade"]}.get(dom, 0)
+             "trace_shade": ef[0] + ef[1] + stats["shade_events"] * FLOPS["shade"],
+             "chain": ef[0] + ef[1] + stats["shade_events"] * FLOPS["shade"]}.get(dom, 0)
     launches_per_step = dom_n / steps
     # flops of one step / (this kernel's time per step) == per-launch flops / average launch duration
     achieved = flops / (dom_ms / steps / 1e3) / 1e12 if dom_ms > 0 else 0.0
@@ -304,7 +316,8 @@ def roofline_of(sess, ktimes, stats, steps, in_region):
     per_ray = FLOPS["sphere"] * c["sphere"] + FLOPS["plane"] * c["plane"] + FLOPS["group"] * c["group"] + FLOPS["tri"] * c["tri"]
     ref_flops = {"trace": stats["rays"] * per_ray, "n1n2": stats["n1n2_scans"] * per_ray,
                  "shade": stats["shadow_rays"] * per_ray + stats["shade_events"] * FLOPS["shade"],
-                 "trace_shade": (stats["rays"] + stats["shadow_rays"]) * per_ray + stats["shade_events"] * FLOPS["shade"]
+                 "trace_shade": (stats["rays"] + stats["shadow_rays"]) * per_ray + stats["shade_events"] * FLOPS["shade"],
+                 "chain": (stats["rays"] + stats["shadow_rays"]) * per_ray + stats["shade_events"] * FLOPS["shade"]
                  }.get(dom, 0)
     ref_tf = ref_flops / (dom_ms / steps / 1e3) / 1e12 if dom_ms > 0 else 0.0
     return {"bound": "valu_fp64", "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -28,7 +28,7 @@ CSG_OPS = {"union": 0, "intersection": 1, "difference": 2}
 PAT = {"test": 0, "solid": 1, "stripe": 2, "gradient": 3, "ring": 4, "checker": 5, "blend": 6, "perturbed": 7,
        "noise": 8, "texture": 9}
 LIGHT_POINT, LIGHT_AREA = 0, 1
-KERNELS = ["trace", "n1n2", "shade", "shadow", "finish", "combine", "aa", "trace_shade", "chain"]
+KERNELS = ["trace", "n1n2", "shade", "shadow", "finish", "combine", "aa", "trace_shade", "chain", "deep"]
 
 _D = C.POINTER(C.c_double)
 _I = C.POINTER(C.c_int32)

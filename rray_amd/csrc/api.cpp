@@ -72,6 +72,7 @@ struct rr_ctx {
     DBuf culls, chunks, nodes, groups, shapes, tris, mats, pats, lights, textures, texels;
     // workspace
     DBuf counters, lcount, hit, n12, n1n2, ev_a, ev_b, canvas, rays0, qout;
+    DBuf deep;  // chain kernels' deep queue (rr::DeepRec, RR_NSEG segments)
     // per-tile camera-ray bundles of the last camera / part layout (tile_bundle_kernel), reused while they match
     DBuf tiles;
     struct TileKey {
@@ -309,7 +310,9 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
         while (rows_unit % aap->aa) rows_unit += 8;
         const int64_t unit = rows_unit * base_args.hs;
         const int64_t units = total / unit;
-        const int np = std::max(1, std::atoi(std::getenv("RRAY_AA_PASSES") ? std::getenv("RRAY_AA_PASSES") : "4"));
+        // default one pass: measured on C3 (chain kernel), 2 / 4 / 8 passes cost 7.29 / 7.61 / 8.01 ms per frame
+        // against 7.08 — each pass ends in its own tail of long chains, and the averages did not overlap it
+        const int np = std::max(1, std::atoi(std::getenv("RRAY_AA_PASSES") ? std::getenv("RRAY_AA_PASSES") : "1"));
         if (total % unit == 0 && units >= 2 && np > 1 && B >= unit) {
             const int64_t per = std::min((units + np - 1) / np, B / unit);
             B = per * unit;
@@ -337,6 +340,11 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
     if (P.ev_cap[0]) HIPCHK(c->ev_a.ensure(P.ev_cap[0] * sizeof(rr::Event)));
     if (P.ev_cap[1]) HIPCHK(c->ev_b.ensure(P.ev_cap[1] * sizeof(rr::Event)));
     unsigned int* lc = c->lcount.as<unsigned int>();
+    // deep chains (chain_kernel DEEP): frames whose samples are delivered one by one (not the in-wave AA average)
+    // send the chains still reflecting at depth RR_DEEP_FROM to a packed, segmented queue for a second launch
+    const bool spill = chain && aa_wave == 0 && max_depth >= rr::RR_DEEP_FROM && !std::getenv("RRAY_NO_DEEP");
+    const int64_t deep_seg_cap = ((((B + 255) / 256) + rr::RR_NSEG - 1) / rr::RR_NSEG) * 256;
+    if (spill) HIPCHK(c->deep.ensure((size_t)rr::RR_NSEG * deep_seg_cap * sizeof(rr::DeepRec)));
     // cost-ordered level-0 tiles: one-batch fused frames of full 8x8 tiles whose level 0 is the whole frame (no
     // secondary rays) in scenes with groups, where tile costs spread widest (mesh silhouettes against floor:
     // C4 0.596 -> 0.511 ms per frame).  Flat scenes' tiles cost alike (C2 +0.6 % with the order), and frames
@@ -368,8 +376,8 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
         const int64_t nb = std::min(B, total - base);
         const LevelPlan p = plan_levels(nb, k, plan_depth, ext, fused);
         // per-level queue counters [level][LC_*], zeroed once per batch (appends, pending, n1/n2 lists)
-        if (p.levels > 1 || ext)
-            HIPCHK(hipMemsetAsync(lc, 0, (size_t)p.levels * rr::LC_COUNT * sizeof(unsigned int), st));
+        if (p.levels > 1 || ext || spill)
+            HIPCHK(hipMemsetAsync(lc, 0, (size_t)std::max(p.levels, 2) * rr::LC_COUNT * sizeof(unsigned int), st));
         for (int d = 0; d < p.levels; ++d) {
             const bool children_possible = d + 1 < p.levels;
             rr::LevelArgs A = base_args;
@@ -416,9 +424,25 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             }
             A.counters = frame_counters(c, c->epoch);
             A.counters_zero = (c->zero_next && d == 0 && base == 0) ? frame_counters(c, c->epoch ^ 1) : nullptr;
-            if (chain)
+            if (chain) {
+                if (spill) {  // camera launch appends to the deep queue's segments (level 1's counters)
+                    A.deep = c->deep.as<rr::DeepRec>();
+                    A.deep_from = rr::RR_DEEP_FROM;
+                    A.nseg_out = rr::RR_NSEG;
+                    A.seg_out_count = lc + rr::LC_COUNT + rr::LC_SEG0;
+                    A.seg_cap_out = deep_seg_cap;
+                }
                 HIPCHK(rr::launch_chain(c->S, A, st, c->profile ? &c->prof : nullptr));
-            else
+                if (spill) {  // the deep launch: one block per segment
+                    rr::LevelArgs D = A;
+                    D.nseg = rr::RR_NSEG;
+                    D.seg_count = A.seg_out_count;
+                    D.seg_cap = deep_seg_cap;
+                    D.seg_out_count = nullptr;
+                    D.counters_zero = nullptr;
+                    HIPCHK(rr::launch_chain(c->S, D, st, c->profile ? &c->prof : nullptr, true));
+                }
+            } else
                 HIPCHK(rr::launch_level(c->S, A, st, c->profile ? &c->prof : nullptr));
             if (order_ok && d == 0 && (!c->order_valid || ++c->order_age >= kRR_ORDER_EVERY)) {
                 HIPCHK(rr::launch_tile_order(c->tile_cost.as<uint32_t>(), c->tile_perm.as<uint32_t>(),
@@ -654,7 +678,7 @@ void rr_destroy(rr_ctx* c) {
     if (c->stream) (void)sync_ctx(c);
     for (DBuf* b : {&c->culls, &c->chunks, &c->nodes, &c->groups, &c->shapes, &c->tris, &c->mats, &c->pats, &c->lights, &c->textures, &c->texels, &c->counters,
                     &c->lcount, &c->hit, &c->n12, &c->n1n2, &c->ev_a, &c->ev_b, &c->canvas, &c->rays0, &c->qout, &c->tiles,
-                    &c->tile_cost, &c->tile_perm, &c->tile_hist})
+                    &c->tile_cost, &c->tile_perm, &c->tile_hist, &c->deep})
         b->release();
     for (auto& b : c->comb) b.release();
     for (auto& b : c->comb_ext) b.release();

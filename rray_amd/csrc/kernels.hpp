@@ -50,6 +50,11 @@ struct LevelArgs {
     const uint32_t* tile_perm;
     uint32_t* tile_cost;
     int32_t pad_children;    // fused levels: children in per-wave 64-slot blocks (holes: Event.parent == -2)
+    // chain kernels (chain_kernel): the deep queue (segmented like the fused levels' queues: the camera launch
+    // appends to seg_out_count / seg_cap_out, the deep launch reads seg_count / seg_cap) and the depth at which
+    // chains leave their camera wave for it (0: they never do)
+    DeepRec* deep;
+    int32_t deep_from;
     int32_t aa_wave;         // 2 / 4 / 8: every pixel's aa x aa samples lie in one wave's 8x8 tile and no
                              // sample has a secondary ray: the wave box-averages and writes avg (0: off)
     int32_t avg_f32;         // avg holds floats (RR_OUT_AVG_F32)
@@ -118,7 +123,7 @@ __host__ __device__ inline uint32_t tile_to_local_u32(uint32_t t, uint32_t hs, u
 
 // Optional per-kernel timing: when `prof` is non-null every launch is bracketed by HIP events on
 // the launch stream and appended to it (resolved on the host after a synchronise).
-enum KernelId { K_TRACE = 0, K_N1N2, K_SHADE, K_SHADOW, K_FINISH, K_COMBINE, K_AA, K_TRACE_SHADE, K_CHAIN, K_COUNT };
+enum KernelId { K_TRACE = 0, K_N1N2, K_SHADE, K_SHADOW, K_FINISH, K_COMBINE, K_AA, K_TRACE_SHADE, K_CHAIN, K_DEEP, K_COUNT };
 struct KernelProf {
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> marks;
     std::vector<hipEvent_t> pool;
@@ -146,8 +151,10 @@ hipError_t launch_combine(const CombArgs& C, hipStream_t stream, KernelProf* pro
 // (render_levels.inc chain_kernel), one launch per batch with no recursion queues
 bool chain_levels(const DevScene& S, int max_children, int max_depth);
 template <int G, bool LC>
-void launch_chain_t(const DevScene& S, const LevelArgs& A, hipStream_t stream, KernelProf* prof);
-hipError_t launch_chain(const DevScene& S, const LevelArgs& A, hipStream_t stream, KernelProf* prof = nullptr);
+void launch_chain_t(const DevScene& S, const LevelArgs& A, hipStream_t stream, KernelProf* prof, bool deep);
+// deep: the deep queue's launch (one block per segment, A.nseg segments), else the camera launch
+hipError_t launch_chain(const DevScene& S, const LevelArgs& A, hipStream_t stream, KernelProf* prof = nullptr,
+                        bool deep = false);
 hipError_t launch_aa(const double* canvas, double* out, int64_t width, int64_t rows, int32_t aa, hipStream_t stream,
                      KernelProf* prof = nullptr);
 hipError_t launch_aa_f32(const double* canvas, float* out, int64_t width, int64_t rows, int32_t aa, hipStream_t stream,

@@ -243,24 +243,24 @@ bool chain_levels(const DevScene& S, int max_children, int max_depth) {
     return fused_levels(S) && max_children > 0 && max_depth > 0 && !std::getenv("RRAY_NO_CHAIN");
 }
 
-hipError_t launch_chain(const DevScene& S, const LevelArgs& A, hipStream_t st, KernelProf* prof) {
+hipError_t launch_chain(const DevScene& S, const LevelArgs& A, hipStream_t st, KernelProf* prof, bool deep) {
     if (A.n <= 0) return hipSuccess;
     const int g = S.general ? 2 : S.has_groups ? 1 : 0;
     if (g == 2) {
         if (S.lds_culls)
-            launch_chain_t<2, true>(S, A, st, prof);
+            launch_chain_t<2, true>(S, A, st, prof, deep);
         else
-            launch_chain_t<2, false>(S, A, st, prof);
+            launch_chain_t<2, false>(S, A, st, prof, deep);
     } else if (g == 1) {
         if (S.lds_culls)
-            launch_chain_t<1, true>(S, A, st, prof);
+            launch_chain_t<1, true>(S, A, st, prof, deep);
         else
-            launch_chain_t<1, false>(S, A, st, prof);
+            launch_chain_t<1, false>(S, A, st, prof, deep);
     } else {
         if (S.lds_culls)
-            launch_chain_t<0, true>(S, A, st, prof);
+            launch_chain_t<0, true>(S, A, st, prof, deep);
         else
-            launch_chain_t<0, false>(S, A, st, prof);
+            launch_chain_t<0, false>(S, A, st, prof, deep);
     }
     return hipGetLastError();
 }

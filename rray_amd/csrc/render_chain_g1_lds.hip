@@ -11,5 +11,5 @@ namespace rr {
 #include "render_common.inc"
 #include "render_levels.inc"
 
-template void launch_chain_t<1, true>(const DevScene&, const LevelArgs&, hipStream_t, KernelProf*);
+template void launch_chain_t<1, true>(const DevScene&, const LevelArgs&, hipStream_t, KernelProf*, bool);
 }  // namespace rr

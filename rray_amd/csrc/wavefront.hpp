@@ -52,6 +52,17 @@ struct alignas(16) ChainRec {
 };
 static_assert(sizeof(ChainRec) == 48 && sizeof(ChainRec) <= sizeof(CombRec), "ChainRec layout");
 enum { CF_HIT = 1, CF_REFRACT_CHILD = 2 };
+// A reflection chain leaving its camera wave at depth RR_DEEP_FROM for the deep launch (render_levels.inc
+// chain_kernel): the pending reflected ray, the chain's records of depths 0 .. RR_DEEP_FROM - 1 (shade_hit's
+// surface sum and the material's reflective), and the camera sample's output index.
+constexpr int RR_DEEP_FROM = 2;
+struct alignas(16) DeepRec {
+    double o[3], d[3];
+    double rec[RR_DEEP_FROM][4];
+    uint32_t ls;
+    uint32_t pad[3];
+};
+static_assert(sizeof(DeepRec) == 128, "DeepRec layout");
 
 // per-level device counters.  Fused levels (no transparency) queue their children in RR_NSEG segments
 // (block b appends to segment b % RR_NSEG with one atomic per wave, no workgroup barrier; the next
