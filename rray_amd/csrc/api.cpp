@@ -72,13 +72,14 @@ struct rr_ctx {
     DBuf culls, chunks, nodes, groups, shapes, tris, mats, pats, lights, textures, texels;
     // workspace
     DBuf counters, lcount, hit, n12, n1n2, ev_a, ev_b, canvas, rays0, qout;
-    DBuf deep;  // chain kernels' deep queue (rr::DeepRec, RR_NSEG segments)
+    DBuf deep, deep_count;  // chain kernels' deep queue (rr::DeepRec segments) and its segment counters
     // per-tile camera-ray bundles of the last camera / part layout (tile_bundle_kernel), reused while they match
     DBuf tiles;
     struct TileKey {
         rr::DevCamera cam;
         int64_t hs, lrows;
         int32_t aa, part, nparts, block_rows;
+        int32_t pw, pad;
     } tile_key{};
     bool tiles_valid = false;
     // level-0 launch order of one-batch fused frames: every wave stores its tile's cost (clock cycles) and the
@@ -220,6 +221,9 @@ LevelPlan plan_levels(int64_t nb, int k, int max_depth, bool ext, bool fused = f
     return p;
 }
 
+// pixel waves of a part (A.pw): bands of two output rows, pw_wpb waves each
+int64_t pixel_waves(const rr::LevelArgs& A) { return (int64_t)((A.pw_rows + 1) / 2) * A.pw_wpb; }
+
 // level-0 index math: magic divisors, and the wave-uniform tile path when every tile is a full 8x8 and the
 // batch starts on a tile boundary
 void set_level0_index(rr::LevelArgs& A) {
@@ -238,10 +242,11 @@ int tile_bundles(rr_ctx* c, const rr::LevelArgs& base_args, hipStream_t st, cons
     T.base = 0;
     T.level = 0;
     set_level0_index(T);
-    if (!T.tile_fast || !T.cam_affine) return RR_OK;
+    if ((!T.tile_fast && !T.pw) || !T.cam_affine) return RR_OK;
     // few-node flat scenes with LDS culls walk node by node without bundles (walk_nodes)
     if (!c->S.has_groups && !c->S.general && c->S.lds_culls && c->S.n_nodes <= rr::RR_BUNDLE_MIN_NODES) return RR_OK;
-    const int64_t n_tiles = T.hs * T.lrows / 64;
+    // one bundle per 8x8 tile, or per pixel wave (A.pw)
+    const int64_t n_tiles = T.pw ? pixel_waves(T) : T.hs * T.lrows / 64;
     const size_t want = (size_t)n_tiles * rr::RR_TILE_BUNDLE_FLOATS * sizeof(float);
     if (want > c->tiles.bytes) {
         HIPCHK(c->tiles.ensure(want));
@@ -255,8 +260,12 @@ int tile_bundles(rr_ctx* c, const rr::LevelArgs& base_args, hipStream_t st, cons
     key.part = T.part;
     key.nparts = T.nparts;
     key.block_rows = T.block_rows;
+    key.pw = T.pw;
     if (!c->tiles_valid || std::memcmp(&key, &c->tile_key, sizeof key) != 0) {
-        HIPCHK(rr::launch_tile_bundles(c->S, T, c->tiles.as<float>(), n_tiles, st));
+        if (T.pw)
+            HIPCHK(rr::launch_pixel_wave_bundles(T, c->tiles.as<float>(), n_tiles, st));
+        else
+            HIPCHK(rr::launch_tile_bundles(c->S, T, c->tiles.as<float>(), n_tiles, st));
         c->tile_key = key;
         c->tiles_valid = true;
     }
@@ -341,10 +350,16 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
     if (P.ev_cap[1]) HIPCHK(c->ev_b.ensure(P.ev_cap[1] * sizeof(rr::Event)));
     unsigned int* lc = c->lcount.as<unsigned int>();
     // deep chains (chain_kernel DEEP): frames whose samples are delivered one by one (not the in-wave AA average)
-    // send the chains still reflecting at depth RR_DEEP_FROM to a packed, segmented queue for a second launch
-    const bool spill = chain && aa_wave == 0 && max_depth >= rr::RR_DEEP_FROM && !std::getenv("RRAY_NO_DEEP");
-    const int64_t deep_seg_cap = ((((B + 255) / 256) + rr::RR_NSEG - 1) / rr::RR_NSEG) * 256;
-    if (spill) HIPCHK(c->deep.ensure((size_t)rr::RR_NSEG * deep_seg_cap * sizeof(rr::DeepRec)));
+    // can send the chains still reflecting at depth RR_DEEP_FROM to a packed, segmented queue for a second launch.
+    // Opt-in (RRAY_DEEP=1): on C3 the deep launch took 1.85 ms for what the camera waves did in 1.54 — the deep
+    // rays' walks are latency-bound whether their waves are full or not
+    const bool spill = chain && aa_wave == 0 && !base_args.pw && max_depth >= rr::RR_DEEP_FROM && std::getenv("RRAY_DEEP") &&
+                       std::atoi(std::getenv("RRAY_DEEP")) == 1;
+    const int64_t deep_seg_cap = (int64_t)256 << rr::RR_DEEP_SHIFT;
+    const int64_t deep_nseg = (((B + 255) / 256) + (1 << rr::RR_DEEP_SHIFT) - 1) >> rr::RR_DEEP_SHIFT;
+    if (spill) HIPCHK(c->deep.ensure((size_t)deep_nseg * deep_seg_cap * sizeof(rr::DeepRec)));
+    if (spill && (size_t)(deep_nseg + 2) * sizeof(unsigned int) > c->deep_count.bytes)
+        HIPCHK(c->deep_count.ensure((size_t)(deep_nseg + 2) * sizeof(unsigned int)));
     // cost-ordered level-0 tiles: one-batch fused frames of full 8x8 tiles whose level 0 is the whole frame (no
     // secondary rays) in scenes with groups, where tile costs spread widest (mesh silhouettes against floor:
     // C4 0.596 -> 0.511 ms per frame).  Flat scenes' tiles cost alike (C2 +0.6 % with the order), and frames
@@ -376,8 +391,9 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
         const int64_t nb = std::min(B, total - base);
         const LevelPlan p = plan_levels(nb, k, plan_depth, ext, fused);
         // per-level queue counters [level][LC_*], zeroed once per batch (appends, pending, n1/n2 lists)
-        if (p.levels > 1 || ext || spill)
-            HIPCHK(hipMemsetAsync(lc, 0, (size_t)std::max(p.levels, 2) * rr::LC_COUNT * sizeof(unsigned int), st));
+        if (p.levels > 1 || ext)
+            HIPCHK(hipMemsetAsync(lc, 0, (size_t)p.levels * rr::LC_COUNT * sizeof(unsigned int), st));
+        if (spill) HIPCHK(hipMemsetAsync(c->deep_count.p, 0, (size_t)deep_nseg * sizeof(unsigned int), st));
         for (int d = 0; d < p.levels; ++d) {
             const bool children_possible = d + 1 < p.levels;
             rr::LevelArgs A = base_args;
@@ -407,6 +423,10 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             A.avg = avg;
             A.avg_f32 = avg_f32;
             A.aa_wave = (d == 0 && A.tile_fast) ? aa_wave : 0;
+            if (A.pw) {  // pixel waves: the launch holds whole waves of 7 pixels (one batch, chain kernels only)
+                if (!chain || B < total) return fail(RR_E_ARG, "internal: pixel waves need one chain-kernel batch");
+                A.n = pixel_waves(A) * 64;
+            }
             // fused levels queue each wave's reflected rays in a 64-slot block of its own, at the lanes they
             // left (holes marked): a secondary wave is one camera tile's rays, as coherent as they come.
             // Packed queues mixed 2-4 tiles per wave (C3 10.54 -> 8.98 ms with the blocks); the area-light
@@ -428,14 +448,14 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
                 if (spill) {  // camera launch appends to the deep queue's segments (level 1's counters)
                     A.deep = c->deep.as<rr::DeepRec>();
                     A.deep_from = rr::RR_DEEP_FROM;
-                    A.nseg_out = rr::RR_NSEG;
-                    A.seg_out_count = lc + rr::LC_COUNT + rr::LC_SEG0;
+                    A.nseg_out = (int32_t)deep_nseg;
+                    A.seg_out_count = c->deep_count.as<unsigned int>();
                     A.seg_cap_out = deep_seg_cap;
                 }
                 HIPCHK(rr::launch_chain(c->S, A, st, c->profile ? &c->prof : nullptr));
                 if (spill) {  // the deep launch: one block per segment
                     rr::LevelArgs D = A;
-                    D.nseg = rr::RR_NSEG;
+                    D.nseg = (int32_t)deep_nseg;
                     D.seg_count = A.seg_out_count;
                     D.seg_cap = deep_seg_cap;
                     D.seg_out_count = nullptr;
@@ -678,7 +698,7 @@ void rr_destroy(rr_ctx* c) {
     if (c->stream) (void)sync_ctx(c);
     for (DBuf* b : {&c->culls, &c->chunks, &c->nodes, &c->groups, &c->shapes, &c->tris, &c->mats, &c->pats, &c->lights, &c->textures, &c->texels, &c->counters,
                     &c->lcount, &c->hit, &c->n12, &c->n1n2, &c->ev_a, &c->ev_b, &c->canvas, &c->rays0, &c->qout, &c->tiles,
-                    &c->tile_cost, &c->tile_perm, &c->tile_hist, &c->deep})
+                    &c->tile_cost, &c->tile_perm, &c->tile_hist, &c->deep, &c->deep_count})
         b->release();
     for (auto& b : c->comb) b.release();
     for (auto& b : c->comb_ext) b.release();
@@ -901,7 +921,10 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     // aa == 1, or aa in {2, 4, 8} without secondary rays (wave_avg_ok): the average is written by the
     // kernels directly; the canvas only when asked for
     const bool wave_avg = d_avg && wave_avg_ok(c, o->aa, cam->hsize, local_rows, o->max_depth);
-    const bool direct_avg = d_avg && (o->aa == 1 || wave_avg);
+    // aa == 3 frames with reflection chains: pixel waves (7 whole pixels per wave) average in the wave too
+    const bool pw = d_avg && !wave_avg && o->aa == 3 && rr::chain_levels(c->S, c->host.max_children, o->max_depth) &&
+                    block % 2 == 0 && total <= c->batch && !std::getenv("RRAY_NO_PW");
+    const bool direct_avg = d_avg && (o->aa == 1 || wave_avg || pw);
     double* canvas = static_cast<double*>(d_canvas);
     if (!canvas && !direct_avg) {
         HIPCHK(c->canvas.ensure(std::max<int64_t>(total, 1) * 3 * sizeof(double)));
@@ -922,6 +945,11 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     A.rays0 = nullptr;
     A.seed = o->seed;
     A.jitter_mode = o->jitter_mode;
+    if (pw) {
+        A.pw = 1;
+        A.pw_rows = (int32_t)rows;
+        A.pw_wpb = (uint32_t)((2 * W + 6) / 7);
+    }
     const int32_t f32 = (o->flags & RR_OUT_AVG_F32) ? 1 : 0;
     rc = tile_bundles(c, A, st, &A.tile_bundles);
     if (rc != RR_OK) return rc;

@@ -55,6 +55,11 @@ struct LevelArgs {
     // chains leave their camera wave for it (0: they never do)
     DeepRec* deep;
     int32_t deep_from;
+    // pixel waves (aa == 3, chain kernels, render_common.inc pixel_wave): level-0 waves of 7 whole pixels, averaged in
+    // the wave; pw_wpb waves per band of two output rows, pw_rows the part's output rows
+    int32_t pw;
+    uint32_t pw_wpb;
+    int32_t pw_rows;
     int32_t aa_wave;         // 2 / 4 / 8: every pixel's aa x aa samples lie in one wave's 8x8 tile and no
                              // sample has a secondary ray: the wave box-averages and writes avg (0: off)
     int32_t avg_f32;         // avg holds floats (RR_OUT_AVG_F32)
@@ -89,7 +94,7 @@ struct CombArgs {
 // stage (scenes with an area light).
 constexpr int RR_PRELIT_LIGHTS = 2;
 constexpr size_t RR_AREA_STAGE_BYTES = 3 * 256 * 8 + 2 * 256 * 4;
-constexpr size_t RR_CHAIN_STAGE_BYTES = 10 * 256 * 8;  // chain kernels: parked reflected ray + level-0 record
+constexpr size_t RR_CHAIN_STAGE_BYTES = 10 * 256 * 8 + 3 * 256 * 4;  // chain kernels: parked ray, level-0 record, Px0
 
 // Level-0 camera events run in 8x8-sample tiles of the part-local supersampled canvas (8-row bands,
 // 8-column tiles inside a band; the last band / column may be narrower) so that a wave's 64 rays
@@ -136,6 +141,8 @@ hipError_t launch_level(const DevScene& S, const LevelArgs& A, hipStream_t strea
 // out (n_tiles x RR_TILE_BUNDLE_FLOATS floats): exactly the bundle make_bundle's cam_tile path builds in the walk.
 constexpr int RR_TILE_BUNDLE_FLOATS = 12;
 hipError_t launch_tile_bundles(const DevScene& S, const LevelArgs& A, float* out, int64_t n_tiles, hipStream_t stream);
+// the same per pixel wave (A.pw): the bundle of the wave's 12 x 6-sample footprint from its corner rays
+hipError_t launch_pixel_wave_bundles(const LevelArgs& A, float* out, int64_t n_waves, hipStream_t stream);
 // perm = tiles by decreasing recorded cost (LevelArgs.tile_cost), for the next frames' level-0 launches;
 // scratch = 256 u32 of device memory (bucket counters)
 hipError_t launch_tile_order(const uint32_t* cost, uint32_t* perm, uint32_t* scratch, int64_t n_tiles, hipStream_t stream);

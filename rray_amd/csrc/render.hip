@@ -119,6 +119,48 @@ __global__ void __launch_bounds__(256) tile_bundle_kernel(LevelArgs A, float* __
     p[10] = p[11] = 0.0f;
 }
 
+// One thread per pixel wave (A.pw): the bundle of the rectangle spanning the wave's samples (the first and last
+// pixel's columns, the band's rows) from its four corner rays — every sample ray of the wave lies in the cone of the
+// rectangle's corner rays (the argument of the 8x8 tiles).
+__global__ void __launch_bounds__(256) pixel_wave_bundle_kernel(LevelArgs A, float* __restrict__ out, int64_t n_waves) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_waves) return;
+    const PixelWave pw = pixel_wave(A, (uint32_t)g);
+    const uint32_t W = (uint32_t)A.hs / 3u;  // output pixels per row
+    const uint32_t p0 = 7u * pw.w, p_end = pw.rb * W - 1u, p1 = p0 + 6u < p_end ? p0 + 6u : p_end;
+    const uint32_t c0 = pw.rb == 2u ? p0 >> 1 : p0, c1 = pw.rb == 2u ? p1 >> 1 : p1;
+    const uint32_t x0 = 3u * c0, x1 = 3u * c1 + 2u;
+    const uint32_t y0 = 6u * pw.band, y1 = y0 + 3u * pw.rb - 1u;
+    const uint32_t cx[4] = {x0, x1, x0, x1}, cy[4] = {y0, y0, y1, y1};
+    float o[3] = {0.0f, 0.0f, 0.0f}, dc[4][3];
+    for (int j = 0; j < 4; ++j) {
+        const Ray r = camera_ray(A.cam, A.cam_affine, cx[j], canvas_row(A, cy[j]));
+        o[0] = (float)r.o.x;
+        o[1] = (float)r.o.y;
+        o[2] = (float)r.o.z;
+        dc[j][0] = (float)r.d.x;
+        dc[j][1] = (float)r.d.y;
+        dc[j][2] = (float)r.d.z;
+    }
+    const Bundle B = cam_corner_bundle(o, dc);
+    float* p = out + g * RR_TILE_BUNDLE_FLOATS;
+    for (int k = 0; k < 3; ++k) {
+        p[k] = B.o[k];
+        p[3 + k] = B.a[k];
+    }
+    p[6] = B.rho;
+    p[7] = B.tanT;
+    p[8] = B.secT;
+    p[9] = __int_as_float(B.ok);
+    p[10] = p[11] = 0.0f;
+}
+
+hipError_t launch_pixel_wave_bundles(const LevelArgs& A, float* out, int64_t n_waves, hipStream_t st) {
+    if (n_waves <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pixel_wave_bundle_kernel, dim3(blocks_for(n_waves)), dim3(256), 0, st, A, out, n_waves);
+    return hipGetLastError();
+}
+
 // Tiles by decreasing cost (a counting sort on 256 buckets: 8 per power of two of the cycle count), so a
 // frame's costliest tiles start first and its last waves are its cheapest: the launch's tail, where CUs run
 // out of waves, shrinks.  Ties in a bucket land in any order (only timing depends on it).  Three small

@@ -56,6 +56,9 @@ enum { CF_HIT = 1, CF_REFRACT_CHILD = 2 };
 // chain_kernel): the pending reflected ray, the chain's records of depths 0 .. RR_DEEP_FROM - 1 (shade_hit's
 // surface sum and the material's reflective), and the camera sample's output index.
 constexpr int RR_DEEP_FROM = 2;
+// deep-queue segments: camera blocks b with equal b >> RR_DEEP_SHIFT append to one segment (neighbouring tiles,
+// so a deep wave's rays come from one stretch of the frame), capacity (256 << RR_DEEP_SHIFT) entries
+constexpr int RR_DEEP_SHIFT = 5;
 struct alignas(16) DeepRec {
     double o[3], d[3];
     double rec[RR_DEEP_FROM][4];

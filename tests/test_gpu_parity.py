@@ -255,18 +255,25 @@ def test_reflection_chains_in_kernel_match_levels(renderer, name, W, H, aa):
     sphere: unfused levels either way)."""
     scene, _ = _yaml_pair(name, W, H, aa)
     renderer.upload(scene)
-    chain = renderer.render(scene.camera, aa=aa, max_depth=5, seed=3, canvas=True)
-    os.environ["RRAY_NO_CHAIN"] = "1"
-    try:
-        levels = renderer.render(scene.camera, aa=aa, max_depth=5, seed=3, canvas=True)
-    finally:
-        del os.environ["RRAY_NO_CHAIN"]
-    assert np.array_equal(chain["canvas"], levels["canvas"]), name
-    assert np.array_equal(chain["avg"], levels["avg"]), name
+
+    def render_with(env):
+        os.environ.update(env)
+        try:
+            return renderer.render(scene.camera, aa=aa, max_depth=5, seed=3, canvas=True)
+        finally:
+            for k in env:
+                del os.environ[k]
+
+    chain = render_with({})
     # timing and the walks' work counts (culling differs between the kernels' walk variants)
     drop = ("kernel_ms", "exact_flops", "wave_visits", "prim_tests", "group_tests", "group_hits")
-    assert {k: v for k, v in chain["stats"].items() if k not in drop} == \
-        {k: v for k, v in levels["stats"].items() if k not in drop}
+    # RRAY_DEEP=1: chains still reflecting at depth 2 finish in the deep-queue launch (frames without in-wave AA)
+    for env in ({"RRAY_NO_CHAIN": "1"}, {"RRAY_DEEP": "1"}):
+        other = render_with(env)
+        assert np.array_equal(chain["canvas"], other["canvas"]), (name, env)
+        assert np.array_equal(chain["avg"], other["avg"]), (name, env)
+        assert {k: v for k, v in chain["stats"].items() if k not in drop} == \
+            {k: v for k, v in other["stats"].items() if k not in drop}, (name, env)
 
 
 @pytest.mark.parametrize("depth", [0, 1, 2, 3, 5, 8])
@@ -281,6 +288,12 @@ def test_mirror_corridor_depths(R, renderer, depth, aa):
     o, cam = build_from_yaml(MIRRORS, W, H, aa)
     renderer.upload(scene)
     got = renderer.render(scene.camera, aa=aa, max_depth=depth, canvas=True)
+    os.environ["RRAY_DEEP"] = "1"  # the deep-queue launch too (aa 1 and 3: samples delivered one by one)
+    try:
+        deep = renderer.render(scene.camera, aa=aa, max_depth=depth, canvas=True)
+    finally:
+        del os.environ["RRAY_DEEP"]
+    assert np.array_equal(deep["canvas"], got["canvas"]) and np.array_equal(deep["avg"], got["avg"])
     canvas, st = o.render(cam, max_depth=depth)
     _compare(got["canvas"], canvas, f"mirrors aa{aa} depth {depth} canvas")
     _compare(got["avg"], o.aa_average(canvas, aa), f"mirrors aa{aa} depth {depth} avg")
@@ -289,6 +302,33 @@ def test_mirror_corridor_depths(R, renderer, depth, aa):
     assert got["stats"]["shade_events"] == st["shade_events"]
     if depth >= 5:  # the corridor really recurses that deep
         assert st["rays"] - st["shadow_rays"] > 3 * W * H * aa * aa
+
+
+@pytest.mark.parametrize("W,H", [(37, 13), (8, 1), (7, 2), (50, 9)])
+def test_pixel_waves_odd_sizes(R, renderer, W, H):
+    """aa = 3 frames with reflection chains average in the wave (pixel waves: 7 whole pixels per wave, bands of two
+    output rows, render_common.inc pixel_wave): widths that leave a band's last wave short, odd row counts (a
+    one-row last band), one-row frames — canvas, image and counters against the oracle, and the image against the
+    aa_kernel path (RRAY_NO_PW=1) bit for bit."""
+    from oracle.scene_yaml import build_from_yaml
+
+    scene = R.YamlScene(MIRRORS, W, H, 3)
+    o, cam = build_from_yaml(MIRRORS, W, H, 3)
+    renderer.upload(scene)
+    got = renderer.render(scene.camera, aa=3, max_depth=5)
+    both = renderer.render(scene.camera, aa=3, max_depth=5, canvas=True)
+    canvas, st = o.render(cam, max_depth=5)
+    _compare(both["canvas"], canvas, f"mirrors {W}x{H} aa3 canvas")
+    _compare(got["avg"], o.aa_average(canvas, 3), f"mirrors {W}x{H} aa3 pixel waves")
+    assert np.array_equal(got["avg"], both["avg"])
+    assert got["stats"]["rays"] == st["rays"] - st["shadow_rays"]
+    assert got["stats"]["shade_events"] == st["shade_events"]
+    os.environ["RRAY_NO_PW"] = "1"
+    try:
+        ref = renderer.render(scene.camera, aa=3, max_depth=5)
+    finally:
+        del os.environ["RRAY_NO_PW"]
+    assert np.array_equal(got["avg"], ref["avg"])
 
 
 @pytest.mark.parametrize("W,H,aa", [(160, 80, 2), (400, 200, 1)])
