@@ -367,9 +367,11 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
     rr::LevelArgs T0 = base_args;
     T0.base = 0;
     set_level0_index(T0);
-    const int64_t n_tiles = T0.tile_fast ? T0.hs * T0.lrows / 64 : 0;
-    const bool order_ok = fused && !chain && c->S.has_groups && !c->S.general && (k == 0 || max_depth == 0) && B >= total && n_tiles > 0 &&
-                          n_tiles * 64 == total && n_tiles < ((int64_t)1 << 31);
+    // chain frames order their camera waves too (tiles or pixel waves; the chains' depths spread tile costs widely)
+    const int64_t n_tiles = T0.pw ? pixel_waves(T0) : T0.tile_fast ? T0.hs * T0.lrows / 64 : 0;
+    const bool order_ok = fused && !c->S.general && B >= total && n_tiles > 0 && n_tiles < ((int64_t)1 << 31) &&
+                          (T0.pw || n_tiles * 64 == total) &&
+                          ((c->S.has_groups && (k == 0 || max_depth == 0)) || (chain && !std::getenv("RRAY_NO_CHAIN_ORDER")));
     if (order_ok) {
         HIPCHK(c->tile_cost.ensure((size_t)n_tiles * sizeof(uint32_t)));
         HIPCHK(c->tile_perm.ensure((size_t)n_tiles * sizeof(uint32_t)));
@@ -381,6 +383,8 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
         key.part = T0.part;
         key.nparts = T0.nparts;
         key.block_rows = T0.block_rows;
+        key.pw = T0.pw;
+        key.pad = chain ? 1 : 0;  // chain and level-0-only frames of one layout keep orders of their own
         if (c->order_tiles != n_tiles || std::memcmp(&key, &c->order_key, sizeof key) != 0) {
             c->order_valid = false;
             c->order_tiles = n_tiles;

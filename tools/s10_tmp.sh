@@ -1,0 +1,7 @@
+set -u
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/t10.log 2>&1; echo "tests rc=$?"; tail -3 gpurun_out/t10.log
+BENCH_ARGS="--workload c3_s1024_reflect --steps 10 --warmup 3 --no-cpu-baseline --no-anchor --no-cold" bash tools/ab_bench.sh "c3||" "c3nopw||RRAY_NO_PW=1" "c3noord||RRAY_NO_CHAIN_ORDER=1" "c3nopwnoord||RRAY_NO_PW=1;RRAY_NO_CHAIN_ORDER=1" 2>&1 | cut -c1-250
+BENCH_ARGS="--workload c5_area_light --steps 10 --warmup 3 --no-cpu-baseline --no-anchor --no-cold" bash tools/ab_bench.sh "c5||" "c5noord||RRAY_NO_CHAIN_ORDER=1" 2>&1 | cut -c1-250
+BENCH_ARGS="--workload c2_s1024 --steps 30 --warmup 5 --no-cpu-baseline --no-anchor --no-cold" bash tools/ab_bench.sh "c2||" 2>&1 | cut -c1-250

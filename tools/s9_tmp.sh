@@ -4,3 +4,4 @@ mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "chain or mirror or pixel_waves or render_matches or golden" > gpurun_out/t9.log 2>&1; echo "tests rc=$?"; tail -2 gpurun_out/t9.log
 BENCH_ARGS="--workload c3_s1024_reflect --steps 10 --warmup 3 --no-cpu-baseline --no-anchor --no-cold" bash tools/ab_bench.sh "c3||" "c3nopw||RRAY_NO_PW=1" 2>&1 | cut -c1-250
 BENCH_ARGS="--workload c5_area_light --steps 10 --warmup 3 --no-cpu-baseline --no-anchor --no-cold" bash tools/ab_bench.sh "c5||" 2>&1 | cut -c1-250
+BENCH_ARGS="--workload c2_s1024 --steps 30 --warmup 5 --no-cpu-baseline --no-anchor --no-cold" bash tools/ab_bench.sh "c2||" 2>&1 | cut -c1-250
