@@ -370,6 +370,7 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
     // chain frames order their camera waves too (tiles or pixel waves; the chains' depths spread tile costs widely)
     const int64_t n_tiles = T0.pw ? pixel_waves(T0) : T0.tile_fast ? T0.hs * T0.lrows / 64 : 0;
     const bool order_ok = fused && !c->S.general && B >= total && n_tiles > 0 && n_tiles < ((int64_t)1 << 31) &&
+                          n_tiles % 4 == 0 &&  // the order permutes groups of a block's four tiles
                           (T0.pw || n_tiles * 64 == total) &&
                           ((c->S.has_groups && (k == 0 || max_depth == 0)) || (chain && !std::getenv("RRAY_NO_CHAIN_ORDER")));
     if (order_ok) {
@@ -389,6 +390,15 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             c->order_valid = false;
             c->order_tiles = n_tiles;
             c->order_key = key;
+        }
+        // a layout's first frame: order by a guess from the camera bundles (launch order left the first frame's
+        // slowest tiles last: C4 0.59 vs 0.51 ms), and re-sort by the measured costs right after it
+        if (!c->order_valid && T0.tile_bundles && !std::getenv("RRAY_NO_TILE_GUESS")) {
+            HIPCHK(rr::launch_tile_guess(c->S, T0.tile_bundles, c->tile_cost.as<uint32_t>(), n_tiles, st));
+            HIPCHK(rr::launch_tile_order(c->tile_cost.as<uint32_t>(), c->tile_perm.as<uint32_t>(),
+                                         c->tile_hist.as<uint32_t>(), n_tiles, st));
+            c->order_valid = true;
+            c->order_age = kRR_ORDER_EVERY - 1;
         }
     }
     for (int64_t base = 0; base < total; base += B) {

@@ -143,6 +143,9 @@ constexpr int RR_TILE_BUNDLE_FLOATS = 12;
 hipError_t launch_tile_bundles(const DevScene& S, const LevelArgs& A, float* out, int64_t n_tiles, hipStream_t stream);
 // the same per pixel wave (A.pw): the bundle of the wave's 12 x 6-sample footprint from its corner rays
 hipError_t launch_pixel_wave_bundles(const LevelArgs& A, float* out, int64_t n_waves, hipStream_t stream);
+// cost = a guess of each tile's cost from its camera bundle (the nodes of the chunks it may reach), for a layout's
+// first frame, before any tile has been timed
+hipError_t launch_tile_guess(const DevScene& S, const float* bundles, uint32_t* cost, int64_t n_tiles, hipStream_t stream);
 // perm = tiles by decreasing recorded cost (LevelArgs.tile_cost), for the next frames' level-0 launches;
 // scratch = 256 u32 of device memory (bucket counters)
 hipError_t launch_tile_order(const uint32_t* cost, uint32_t* perm, uint32_t* scratch, int64_t n_tiles, hipStream_t stream);

@@ -161,6 +161,30 @@ hipError_t launch_pixel_wave_bundles(const LevelArgs& A, float* out, int64_t n_w
     return hipGetLastError();
 }
 
+// A first frame's tile order before any tile has been timed: each tile's cost is guessed from its camera bundle as
+// 16 + the number of nodes in the chunks its bundle may reach (the walk's candidates), on the clock-cycle scale the
+// counting sort buckets logarithmically (x 64).  Only the launch order depends on it; the frame after re-sorts by
+// the measured costs.  One thread per tile (or pixel wave).
+__global__ void __launch_bounds__(256) tile_guess_kernel(DevScene S, const float* __restrict__ bundles,
+                                                         uint32_t* __restrict__ cost, int64_t n_tiles) {
+    const int64_t T = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (T >= n_tiles) return;
+    const Bundle B = load_tile_bundle(bundles + T * RR_TILE_BUNDLE_FLOATS);
+    uint32_t c = 16u;
+    const int nch = S.n_chunks - S.n_free;
+    for (int j = 0; j < nch; ++j) {
+        const DevChunk ch = S.chunks[j];
+        if (!B.ok || bundle_may_hit<false, true>(B, ch.cull)) c += (uint32_t)ch.count;
+    }
+    cost[T] = c * 64u;
+}
+
+hipError_t launch_tile_guess(const DevScene& S, const float* bundles, uint32_t* cost, int64_t n_tiles, hipStream_t st) {
+    if (n_tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tile_guess_kernel, dim3(blocks_for(n_tiles)), dim3(256), 0, st, S, bundles, cost, n_tiles);
+    return hipGetLastError();
+}
+
 // Tiles by decreasing cost (a counting sort on 256 buckets: 8 per power of two of the cycle count), so a
 // frame's costliest tiles start first and its last waves are its cheapest: the launch's tail, where CUs run
 // out of waves, shrinks.  Ties in a bucket land in any order (only timing depends on it).  Three small
@@ -174,6 +198,15 @@ __device__ __forceinline__ int cost_bucket(uint32_t c) {
     return 255 - (q > 255 ? 255 : q);
 }
 constexpr int RR_ORDER_BLOCK = 256, RR_ORDER_PER_THREAD = 16;  // 4096 tiles per block
+// the launch blocks' units: groups of RR_ORDER_GROUP consecutive tiles (a block's four waves), whose cost is the
+// sum of their tiles' (saturating)
+constexpr int RR_ORDER_GROUP = 4;
+__device__ __forceinline__ uint32_t group_cost(const uint32_t* cost, int64_t g) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int k = 0; k < RR_ORDER_GROUP; ++k) c += cost[g * RR_ORDER_GROUP + k];
+    return c > 0xffffffffull ? 0xffffffffu : (uint32_t)c;
+}
 __global__ void __launch_bounds__(RR_ORDER_BLOCK) tile_hist_kernel(const uint32_t* __restrict__ cost,
                                                                    uint32_t* __restrict__ hist, int64_t n) {
     __shared__ uint32_t h[256];
@@ -182,7 +215,7 @@ __global__ void __launch_bounds__(RR_ORDER_BLOCK) tile_hist_kernel(const uint32_
     const int64_t b0 = (int64_t)blockIdx.x * RR_ORDER_BLOCK * RR_ORDER_PER_THREAD;
     for (int k = 0; k < RR_ORDER_PER_THREAD; ++k) {
         const int64_t i = b0 + (int64_t)k * RR_ORDER_BLOCK + threadIdx.x;
-        if (i < n) atomicAdd(&h[cost_bucket(cost[i])], 1u);
+        if (i < n) atomicAdd(&h[cost_bucket(group_cost(cost, i))], 1u);
     }
     __syncthreads();
     if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
@@ -212,7 +245,7 @@ __global__ void __launch_bounds__(RR_ORDER_BLOCK) tile_scatter_kernel(const uint
 #pragma unroll
     for (int k = 0; k < RR_ORDER_PER_THREAD; ++k) {
         const int64_t i = b0 + (int64_t)k * RR_ORDER_BLOCK + threadIdx.x;
-        bk[k] = i < n ? cost_bucket(cost[i]) : -1;
+        bk[k] = i < n ? cost_bucket(group_cost(cost, i)) : -1;
         if (bk[k] >= 0) atomicAdd(&h[bk[k]], 1u);
     }
     __syncthreads();
@@ -228,9 +261,11 @@ __global__ void __launch_bounds__(RR_ORDER_BLOCK) tile_scatter_kernel(const uint
     }
 }
 
-// scratch: 256 u32 of device memory for the bucket counters
+// scratch: 256 u32 of device memory for the bucket counters; perm: launch block -> tile group (n_tiles a multiple of
+// RR_ORDER_GROUP)
 hipError_t launch_tile_order(const uint32_t* cost, uint32_t* perm, uint32_t* scratch, int64_t n_tiles, hipStream_t st) {
     if (n_tiles <= 0) return hipSuccess;
+    n_tiles /= RR_ORDER_GROUP;  // the sort's units: tile groups
     const unsigned blocks = (unsigned)((n_tiles + RR_ORDER_BLOCK * RR_ORDER_PER_THREAD - 1) / (RR_ORDER_BLOCK * RR_ORDER_PER_THREAD));
     hipError_t e = hipMemsetAsync(scratch, 0, 256 * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
