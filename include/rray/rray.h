@@ -176,9 +176,9 @@ int rr_scene_upload(rr_ctx* ctx, const rr_scene_desc* desc);
 
 /* ---- multi-device contexts (ABI 5): one frame across several GPUs (camera.rs:107-121 spreads one
  * frame over every rayon worker).  Global rank r renders the output rows {y : (y/block_rows) % N == r}
- * as an f64 AA-averaged tile; one RCCL gather (ncclGather over xGMI) brings the tiles to rank 0,
- * which un-interleaves them into frame order.  The context owns a render and a gather stream per
- * device and the RCCL communicator.  rr_render (blocking; out_avg filled on rank 0 only) and
+ * as an f64 AA-averaged tile; one RCCL group of point-to-point operations (over xGMI) brings every
+ * 8-row run of every tile straight into its frame rows on rank 0 (no permutation pass).  The context
+ * owns a render and a transfer stream per device and the RCCL communicator.  rr_render (blocking; out_avg filled on rank 0 only) and
  * rr_render_gather_device (asynchronous) take part 0 of 1: the context does the split.  Only the
  * f64 averaged image is produced (no RR_OUT_CANVAS / RR_OUT_AVG_F32).  rr_color_at / rr_is_shadowed /
  * rr_kernel_times act on the context's first local device; rr_last_stats sums its local devices. */
@@ -192,12 +192,12 @@ int rr_create_rank(int device, int nranks, int rank, const uint8_t* unique_id, r
 /* nranks in the group, this context's first global rank, devices this context drives (1/0/1 for rr_create) */
 int rr_context_info(const rr_ctx* ctx, int32_t* nranks, int32_t* rank, int32_t* ndevices);
 /* ABI 7: nparts VIRTUAL ranks on one device — the N > 1 path of a real group (per-part contexts and
- * streams, padded tiles, the receive buffer in ncclGather's layout, double buffering, the un-interleave
- * kernel) with the transfer replaced by device-local copies.  For exercising / testing the multi-GPU
+ * streams, tiles, double buffering) with the RCCL transfer replaced by a device-local copy of every run
+ * into its frame rows.  For exercising / testing the multi-GPU
  * frame assembly on one GPU; images are bit-identical to one part's. */
 int rr_create_virtual(int device, int nparts, rr_ctx** out);
-/* ABI 7: host restatement of the root's un-interleave (the same index arithmetic as the device kernel):
- * gathered = nparts tiles back to back, each rr_part_rows(height, 0, nparts, block_rows, NULL) rows of
+/* ABI 7: the frame from tiles a caller gathered itself (e.g. torch.distributed.gather; the same run
+ * arithmetic as the device transfer): gathered = nparts tiles back to back, each rr_part_rows(height, 0, nparts, block_rows, NULL) rows of
  * width*3 doubles (part p's rows in increasing y, padded) -> frame = height rows in frame order.  No
  * device needed (CPU rehearsals of the N > 1 path use it).  The buffers are not checked: `gathered` must
  * hold nparts * tile_rows * width * 3 doubles and `frame` height * width * 3 (rray_amd.unshuffle checks

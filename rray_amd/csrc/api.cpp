@@ -897,9 +897,10 @@ int rr_unshuffle_host(const double* gathered, double* frame, int64_t width, int6
     if (!gathered || !frame || width < 0 || height < 0 || nparts < 1 || block < 1)
         return fail(RR_E_ARG, "rr_unshuffle_host: bad arguments");
     const int64_t tile_rows = rr::gather_tile_rows(height, nparts, block), row = width * 3;
-    for (int64_t y = 0; y < height; ++y)
-        std::memcpy(frame + y * row, gathered + rr::gathered_row_of(y, nparts, block, tile_rows) * row,
-                    (size_t)row * sizeof(double));
+    for (int32_t p = 0; p < nparts; ++p)  // the runs rank 0's receives place (partition.hpp)
+        rr::for_each_part_run(height, p, nparts, block, [&](int64_t j, int64_t y, int64_t n) {
+            std::memcpy(frame + y * row, gathered + (p * tile_rows + j) * row, (size_t)(n * row) * sizeof(double));
+        });
     return RR_OK;
 }
 

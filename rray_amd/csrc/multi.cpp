@@ -1,19 +1,22 @@
-// multi.cpp — multi-device render contexts: row-interleaved tiles + one RCCL gather.
+// multi.cpp — multi-device render contexts: row-interleaved tiles received straight into frame order
+// (DESIGN.md §5).
 //
 // Camera::render (camera.rs:107-121) spreads one frame over every rayon worker; here one frame is
 // spread over GPUs.  Global rank r renders the output rows {y : (y / block) % nranks == r} (the
-// interleaving balances sky and floor cost) as an f64 AA-averaged tile in its own HBM, padded to
-// the largest part's row count; one ncclGather (RCCL over xGMI) brings the tiles to rank 0, whose
-// own tile is rendered in place into the gather buffer, and a small kernel un-interleaves them into
-// frame order.  Two tile buffers alternate so that rendering frame k+1 overlaps the gather of frame
-// k: a render waits only for the gather that last read its buffer.  Each part also alternates between
-// two render contexts (scene copy + level workspace) on two render streams, so frame k+1's camera level
-// runs beside frame k's deep levels, whose few incoherent waves leave the GPU mostly idle (with a row
-// tile of C3 per GPU the deep levels are a latency floor per frame, tools/part_scaling.py).
+// interleaving balances sky and floor cost) as an f64 AA-averaged tile in its own HBM.  The tile is a
+// sequence of runs (one 8-row block each) that are contiguous in the frame, so the transfer needs no
+// permutation pass: inside one RCCL group every rank sends its runs to rank 0 (ncclSend, over xGMI) and
+// rank 0 posts one ncclRecv per run of every part straight into that run's frame rows — its own part
+// included, as a send to itself.  Two tile buffers alternate so that rendering frame k+1 overlaps the
+// transfer of frame k: a render waits only for the transfer that last read its buffer.  Each part also
+// alternates between two render contexts (scene copy + level workspace) on two render streams, so frame
+// k+1's camera level runs beside frame k's deep levels, whose few incoherent waves leave the GPU mostly idle
+// (with a row tile of C3 per GPU the deep levels are a latency floor per frame, tools/part_scaling.py).
 //
 // Two shapes of the same group: rr_create_multi (this process drives n devices, ncclCommInitAll,
-// ncclGroupStart/End around the per-device gathers) and rr_create_rank (one process per GPU,
-// ncclCommInitRank from an id made by rr_rccl_unique_id on rank 0 and shared by the host).
+// ncclGroupStart/End around every device's operations) and rr_create_rank (one process per GPU,
+// ncclCommInitRank from an id made by rr_rccl_unique_id on rank 0 and shared by the host).  A virtual group
+// (rr_create_virtual: every part on one device) places each tile's runs with a copy kernel instead.
 #include "multi.hpp"
 
 #include <hip/hip_runtime.h>
@@ -66,23 +69,23 @@ struct DevMem {
     }
 };
 
-// Gathered tiles -> frame order (partition.hpp: the same index arithmetic as rr_unshuffle_host).  One
-// thread per double; both sides are contiguous along a row.
-__global__ void __launch_bounds__(256) unshuffle_kernel(const double* __restrict__ in, double* __restrict__ out,
-                                                        int64_t row_len, int64_t height, int32_t nparts, int32_t block,
-                                                        int64_t max_rows) {
+// A tile's rows -> their frame rows (partition.hpp frame_row_of): the virtual group's transfer.  One thread
+// per double; both sides are contiguous along a row.
+__global__ void __launch_bounds__(256) place_tile_kernel(const double* __restrict__ tile, double* __restrict__ out,
+                                                         int64_t row_len, int64_t rows, int32_t part, int32_t nparts,
+                                                         int32_t block) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= row_len * height) return;
-    const int64_t y = i / row_len, x = i - y * row_len;
-    out[i] = in[rr::gathered_row_of(y, nparts, block, max_rows) * row_len + x];
+    if (i >= row_len * rows) return;
+    const int64_t j = i / row_len, x = i - j * row_len;
+    out[rr::frame_row_of(j, part, nparts, block) * row_len + x] = tile[i];
 }
 
-hipError_t launch_unshuffle(const double* in, double* out, int64_t W, int64_t H, int32_t nparts, int32_t block,
-                            int64_t max_rows, hipStream_t st) {
-    const int64_t n = W * 3 * H;
+hipError_t launch_place_tile(const double* tile, double* out, int64_t W, int64_t rows, int32_t part, int32_t nparts,
+                             int32_t block, hipStream_t st) {
+    const int64_t n = W * 3 * rows;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(unshuffle_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, out, W * 3, H,
-                       nparts, block, max_rows);
+    hipLaunchKernelGGL(place_tile_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, tile, out, W * 3, rows,
+                       part, nparts, block);
     return hipGetLastError();
 }
 
@@ -95,17 +98,16 @@ struct rr_group {
     std::vector<ncclComm_t> comms;
     std::vector<hipStream_t> render_st[2], comm_st;
     std::vector<hipEvent_t> ev_rendered[2], ev_gathered[2];
-    bool virt = false;                    // rr_create_virtual: every part on one device, gather = local copies
+    bool virt = false;                    // rr_create_virtual: every part on one device, transfer = local copies
     hipEvent_t ev_caller = nullptr;       // root: the caller's stream position at the gather call
-    std::vector<DevMem> tile[2];          // non-root local parts: their tile; root: unused
-    DevMem recv[2];                       // root: nranks x padded tile (slot 0 = its own tile, in place)
+    std::vector<DevMem> tile[2];          // per local part: its tile (rows of the part, in tile order)
     DevMem frame;                         // root: assembled frame for the blocking rr_render
     int64_t k = 0;                        // frames issued (buffer and render context = k % 2)
     int nlocal() const { return (int)devices.size(); }
     int last() const { return k > 0 ? (int)((k - 1) & 1) : 0; }  // the set that rendered the latest frame
     bool root_here() const { return rank0 == 0; }
-    // the stream that gathers part l's tile (and releases its buffer): its own comm stream, or for a
-    // virtual group root's, where the copies into the receive buffer run
+    // the stream that transfers part l's tile (and releases its buffer): its own comm stream, or for a
+    // virtual group the root's, where the copies into the frame run
     hipStream_t gather_stream(int l) const { return virt ? comm_st[0] : comm_st[l]; }
 };
 
@@ -248,7 +250,6 @@ void group_destroy(rr_group* g) {
             if (l < g->render_st[b].size() && g->render_st[b][l]) (void)hipStreamDestroy(g->render_st[b][l]);
         if (l < g->comm_st.size() && g->comm_st[l]) (void)hipStreamDestroy(g->comm_st[l]);
         if (l == 0 && g->root_here()) {
-            for (int b = 0; b < 2; ++b) g->recv[b].release();
             g->frame.release();
             if (g->ev_caller) (void)hipEventDestroy(g->ev_caller);
         }
@@ -284,13 +285,11 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
         return gfail(RR_E_ARG, "camera size must be a positive multiple of aa");
     if (g->root_here() && !d_frame) return gfail(RR_E_ARG, "rank 0 needs a device frame buffer");
     const int32_t block = o->block_rows > 0 ? o->block_rows : 8;
-    const int64_t W = cam->hsize / o->aa, H = cam->vsize / o->aa;
-    const int64_t max_rows = gather_tile_rows(H, g->nranks, block);
-    const size_t count = (size_t)max_rows * (size_t)W * 3;  // doubles per (padded) tile
+    const int64_t W = cam->hsize / o->aa, H = cam->vsize / o->aa, row = W * 3;
     const int b = (int)(g->k & 1);
     const int n = g->nlocal();
     // every part's options and buffers are checked / allocated before any work is enqueued: a failure
-    // here returns before this rank joins the collective, never between its render and its gather
+    // here returns before this rank joins the collective, never between its render and its transfer
     std::vector<rr_render_opts> opts(n, *o);
     for (int l = 0; l < n; ++l) {
         rr_render_opts& so = opts[l];
@@ -301,10 +300,7 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
         int rc = render_validate(g->subs[b][l], cam, &so);
         if (rc != RR_OK) return rc;
         GHIP(hipSetDevice(g->devices[l]));
-        if (g->root_here() && l == 0)
-            GHIP(g->recv[b].ensure(count * g->nranks * sizeof(double)));
-        else
-            GHIP(g->tile[b][l].ensure(count * sizeof(double)));
+        GHIP(g->tile[b][l].ensure((size_t)part_rows_count(H, so.part, g->nranks, block) * (size_t)row * sizeof(double)));
     }
     if (g->root_here() && stream) {
         GHIP(hipSetDevice(g->devices[0]));
@@ -312,46 +308,51 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
     }
     for (int l = 0; l < n; ++l) {
         GHIP(hipSetDevice(g->devices[l]));
-        const bool root = g->root_here() && l == 0;
-        void* t = root ? g->recv[b].p : g->tile[b][l].p;
-        // the gather that last read this buffer (two frames ago) must be done before it is overwritten; the
+        // the transfer that last read this buffer (two frames ago) must be done before it is overwritten; the
         // render context and stream of set b are free once that frame's render is (same stream)
         GHIP(hipStreamWaitEvent(g->render_st[b][l], g->ev_gathered[b][l], 0));
-        int rc = rr_render_device(g->subs[b][l], cam, &opts[l], nullptr, t, g->render_st[b][l]);
+        int rc = rr_render_device(g->subs[b][l], cam, &opts[l], nullptr, g->tile[b][l].p, g->render_st[b][l]);
         if (rc != RR_OK) return rc;
         GHIP(hipEventRecord(g->ev_rendered[b][l], g->render_st[b][l]));
         GHIP(hipStreamWaitEvent(g->gather_stream(l), g->ev_rendered[b][l], 0));
     }
-    if (g->virt) {
-        // rank 0's receive buffer in ncclGather's layout: part l's tile at offset l * count (part 0 in place)
+    double* frame = static_cast<double*>(d_frame);
+    if (g->root_here() && stream) {  // d_frame is written in the caller's stream order
         GHIP(hipSetDevice(g->devices[0]));
-        for (int l = 1; l < n; ++l)
-            GHIP(hipMemcpyAsync(static_cast<double*>(g->recv[b].p) + (size_t)l * count, g->tile[b][l].p,
-                                count * sizeof(double), hipMemcpyDeviceToDevice, g->comm_st[0]));
+        GHIP(hipStreamWaitEvent(g->comm_st[0], g->ev_caller, 0));
+    }
+    if (g->virt) {
+        GHIP(hipSetDevice(g->devices[0]));
+        for (int l = 0; l < n; ++l)
+            GHIP(launch_place_tile(static_cast<const double*>(g->tile[b][l].p), frame, W,
+                                   part_rows_count(H, l, g->nranks, block), l, g->nranks, block, g->comm_st[0]));
     } else {
-        // one gather per frame: rank 0 receives rank r's tile at offset r * count (its own in place).  The
-        // RCCL group is always closed, also when a gather call fails.
+        // one RCCL group per frame: each local part sends its runs to rank 0, and rank 0 receives every part's
+        // runs (its own from itself) into their frame rows.  Both sides enumerate the runs with
+        // for_each_part_run, so the operations between a pair of ranks pair up in order.  The group is always
+        // closed, also when posting an operation fails.
         ncclResult_t r = ncclGroupStart();
         if (r == ncclSuccess) {
             for (int l = 0; l < n && r == ncclSuccess; ++l) {
-                const bool root = g->root_here() && l == 0;
-                void* send = root ? g->recv[b].p : g->tile[b][l].p;
-                r = ncclGather(send, root ? g->recv[b].p : nullptr, count, ncclFloat64, 0, g->comms[l], g->comm_st[l]);
+                const double* t = static_cast<const double*>(g->tile[b][l].p);
+                for_each_part_run(H, g->rank0 + l, g->nranks, block, [&](int64_t j, int64_t, int64_t rows) {
+                    if (r == ncclSuccess)
+                        r = ncclSend(t + j * row, (size_t)(rows * row), ncclFloat64, 0, g->comms[l], g->comm_st[l]);
+                });
+                if (!(g->root_here() && l == 0)) continue;
+                for (int32_t p = 0; p < g->nranks && r == ncclSuccess; ++p)
+                    for_each_part_run(H, p, g->nranks, block, [&](int64_t, int64_t y, int64_t rows) {
+                        if (r == ncclSuccess)
+                            r = ncclRecv(frame + y * row, (size_t)(rows * row), ncclFloat64, p, g->comms[0],
+                                         g->comm_st[0]);
+                    });
             }
             const ncclResult_t e = ncclGroupEnd();
             if (r == ncclSuccess) r = e;
         }
-        if (r != ncclSuccess) return gfail(RR_E_HIP, std::string("ncclGather: ") + ncclGetErrorString(r));
+        if (r != ncclSuccess) return gfail(RR_E_HIP, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
     }
-    for (int l = 0; l < n; ++l) {
-        GHIP(hipSetDevice(g->devices[l]));
-        if (g->root_here() && l == 0) {
-            if (stream) GHIP(hipStreamWaitEvent(g->comm_st[0], g->ev_caller, 0));  // d_frame in the caller's order
-            GHIP(launch_unshuffle(static_cast<const double*>(g->recv[b].p), static_cast<double*>(d_frame), W, H,
-                                  g->nranks, block, max_rows, g->comm_st[0]));
-        }
-    }
-    for (int l = 0; l < n; ++l) {  // after the unshuffle: a virtual group's buffers are all read on comm_st[0]
+    for (int l = 0; l < n; ++l) {  // a virtual group's tiles are all read on comm_st[0]
         GHIP(hipSetDevice(g->devices[l]));
         GHIP(hipEventRecord(g->ev_gathered[b][l], g->gather_stream(l)));
     }

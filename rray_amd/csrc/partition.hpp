@@ -33,4 +33,19 @@ __host__ __device__ inline int64_t gathered_row_of(int64_t y, int32_t nparts, in
     return p * tile_rows + j;
 }
 
+// tile row j of part `part` -> its output row (the inverse of gathered_row_of within one tile)
+__host__ __device__ inline int64_t frame_row_of(int64_t j, int32_t part, int32_t nparts, int32_t block) {
+    return ((j / block) * nparts + part) * (int64_t)block + j % block;
+}
+
+// The runs of part `part`'s tile: f(first tile row, first output row, rows) for each interleave block it owns,
+// in tile order.  Sender and receiver of the frame transfer enumerate the same runs, so their point-to-point
+// operations pair up in order (multi.cpp); rr_unshuffle_host copies the same runs on the CPU.
+template <class F>
+inline void for_each_part_run(int64_t height, int32_t part, int32_t nparts, int32_t block, F&& f) {
+    const int64_t rows = part_rows_count(height, part, nparts, block);
+    for (int64_t j = 0; j < rows; j += block)
+        f(j, frame_row_of(j, part, nparts, block), rows - j < block ? rows - j : (int64_t)block);
+}
+
 }  // namespace rr

@@ -4,8 +4,8 @@ Pixels are independent (camera.rs:110-118 renders them in any order), so rank r 
 rows {y : (y // block) % N == r} (interleaved blocks balance sky/floor cost) and one collective
 (torch.distributed.gather; backend "nccl" is RCCL over xGMI on ROCm, "gloo" on CPU tests) brings
 the tiles to rank 0, which scatters the rows back into frame order.  The gather buffer layout and the
-un-interleave are the library's (partition.hpp, rr_unshuffle_host): the same arithmetic as the C ABI's
-own multi-GPU path (multi.cpp), so CPU rehearsals of this module exercise it.
+un-interleave are the library's (partition.hpp, rr_unshuffle_host): the same runs as the C ABI's own
+multi-GPU path places (multi.cpp), so CPU rehearsals of this module exercise that arithmetic.
 
 FramePipeline double-buffers the tiles so that rendering frame k+1 overlaps the gather of frame k
 (the gather runs on the process group's own stream; the renderer waits only for the gather that
@@ -29,8 +29,8 @@ def max_tile_rows(height, world, block=8):
 
 def gather_sources(height, world, block=8):
     """For every output row y, its row in the gathered buffer (world tiles of max_tile_rows rows back
-    to back, ncclGather's layout), computed by the library's own un-interleave (rr_unshuffle_host, the
-    index arithmetic of multi.cpp's device kernel) applied to a buffer whose rows hold their indices."""
+    to back, torch.distributed.gather's layout), computed by the library's own run placement
+    (rr_unshuffle_host, the runs of multi.cpp's transfer) applied to a buffer whose rows hold their indices."""
     rows = max_tile_rows(height, world, block)
     idx = np.repeat(np.arange(world * rows, dtype=np.float64), 3).reshape(world * rows, 1, 3)
     return unshuffle(idx, height, world, block)[:, 0, 0].astype(np.int64)
@@ -38,8 +38,8 @@ def gather_sources(height, world, block=8):
 
 def gather_frame(tile, height, block=8, dst=0, group=None, out=None):
     """tile: (max_tile_rows, W, C) with this rank's rows first (padding after).  One gather into a
-    contiguous (world * max_tile_rows, W, C) buffer on `dst` — the layout multi.cpp's ncclGather
-    produces — then the library's un-interleave.  Returns the (height, W, C) frame on `dst` (written
+    contiguous (world * max_tile_rows, W, C) buffer on `dst`, then the library's run placement
+    (rr_unshuffle_host: the runs multi.cpp's receives place on the device).  Returns the (height, W, C) frame on `dst` (written
     into `out` when given), None on the other ranks."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)

@@ -1,12 +1,12 @@
-"""GPU tests of the multi-device contexts (rr_create_multi / rr_create_rank: row tiles + one RCCL
-gather) and of the drop-in CLI end to end (main.rs:49-77 -> PNG on disk).
+"""GPU tests of the multi-device contexts (rr_create_multi / rr_create_rank: row tiles received straight into
+frame order) and of the drop-in CLI end to end (main.rs:49-77 -> PNG on disk).
 
 The GPU box has one MI355X, so the RCCL groups here have one device / one rank: they exercise the whole
-path through the C ABI (tile render into the gather buffer, ncclGather on a 1-rank communicator, the
-un-interleave kernel, double-buffered pipelining).  The N > 1 frame assembly runs through virtual groups
-(rr_create_virtual): N parts on the one device, each with its own context and streams, padded tiles
-copied into rank 0's receive buffer in ncclGather's layout, the un-interleave kernel with nparts = N —
-everything of the N > 1 path except the RCCL transfer itself.
+path through the C ABI (tile render, one RCCL group of per-run ncclSend / ncclRecv — rank 0 sends its own
+runs to itself — into the frame rows, double-buffered pipelining).  The N > 1 frame assembly runs through
+virtual groups (rr_create_virtual): N parts on the one device, each with its own context and streams, every
+tile's runs placed into the frame by a copy kernel with nparts = N — everything of the N > 1 path except
+the RCCL transfer between devices.
 """
 import ctypes
 import os
@@ -63,12 +63,12 @@ def test_group_context_matches_single_device(R, single, kind):
         g.close()
 
 
-@pytest.mark.parametrize("nparts", [2, 3, 8])
-def test_virtual_group_assembles_the_frame(R, single, nparts):
-    """N virtual ranks (row tiles, padded gather layout, un-interleave kernel with nparts = N) reassemble
-    the 1-part image bit for bit.  40 output rows = 5 blocks of 8: not a multiple of 8N for any N here,
-    so tiles are padded, and at N = 8 three parts own no rows at all.  C3's scene (reflection chains,
-    depth 5) at its own AA."""
+@pytest.mark.parametrize("nparts,block", [(2, 8), (3, 8), (8, 8), (3, 3), (2, 1)])
+def test_virtual_group_assembles_the_frame(R, single, nparts, block):
+    """N virtual ranks (row tiles, each tile's runs placed into their frame rows with nparts = N) reassemble
+    the 1-part image bit for bit.  40 output rows = 5 blocks of 8: not a multiple of 8N for any N here, so
+    parts own different row counts, and at N = 8 three parts own no rows at all; 3-row blocks end in a
+    partial run.  C3's scene (reflection chains, depth 5) at its own AA."""
     W, H, aa = 48, 40, 3
     scene = _scene(R, "c3_s1024_reflect.yaml", W, H, aa)
     single.upload(scene)
@@ -77,7 +77,7 @@ def test_virtual_group_assembles_the_frame(R, single, nparts):
     try:
         assert g.info() == (nparts, 0, nparts)
         g.upload(scene)
-        got = g.render(scene.camera, aa=aa)
+        got = g.render(scene.camera, aa=aa, block_rows=block)
         assert np.array_equal(got["avg"], ref["avg"])
         for k in ("rays", "shadow_rays", "shade_events", "samples"):
             assert got["stats"][k] == ref["stats"][k], k
@@ -85,9 +85,27 @@ def test_virtual_group_assembles_the_frame(R, single, nparts):
         g.close()
 
 
+@pytest.mark.parametrize("block", [1, 3, 8])
+def test_rccl_group_receives_runs_in_frame_order(R, single, block):
+    """The 1-device RCCL group at several block sizes: 40 output rows arrive as 40, 14 or 5 runs (one
+    ncclSend to itself and one ncclRecv into the frame rows per run, the last 3-row run partial), bit for bit
+    the plain context's image."""
+    scene = _scene(R, "c3_s1024_reflect.yaml", 48, 40, 1)
+    single.upload(scene)
+    ref = single.render(scene.camera, aa=1)
+    g = R.Renderer.multi([0])
+    try:
+        g.upload(scene)
+        for _ in range(2):  # the second frame renders into the other tile buffer and context
+            got = g.render(scene.camera, aa=1, block_rows=block)
+            assert np.array_equal(got["avg"], ref["avg"])
+    finally:
+        g.close()
+
+
 def test_virtual_group_pipelined_frames(R, single):
     """rr_render_gather_device on 3 virtual ranks: three frames from two cameras enqueued back to back
-    (double-buffered tiles and receive buffers) land in their own buffers unchanged."""
+    (double-buffered tiles) land in their own buffers unchanged."""
     hip = ctypes.CDLL("libamdhip64.so.7")
     W, H, aa = 64, 44, 2
     scene = _scene(R, "c3_s1024_reflect.yaml", W, H, aa)
