@@ -122,6 +122,9 @@ def main():
                     help="CPU sample: one 8-row band in every STRIDE bands (default sized to ~10-30 s)")
     ap.add_argument("--no-anchor", action="store_true", help="N=1: skip the C3 scaling anchor")
     ap.add_argument("--no-cold", action="store_true", help="N=1: skip the cold-frame measurements")
+    ap.add_argument("--in-flight", type=int, default=2,
+                    help="whole-frame steps: frames alternate over this many render contexts and streams (1 = "
+                         "one frame at a time; N=1 lines with more also time 1 as `serial`)")
     ap.add_argument("--max-depth", type=int, default=None,
                     help="experiment: override the workload's recursion depth (the line then names it in config)")
     ap.add_argument("--kernel-events", choices=("separate", "timed"), default="separate",
@@ -151,11 +154,39 @@ def main():
     return gpu_bench(args, world, mode, workload)
 
 
+class Contexts:
+    """The render contexts a Session alternates its frames over, seen as one for profiling and statistics."""
+
+    def __init__(self, rends):
+        self.rends = rends
+        self.last = 0  # the context that rendered the latest frame
+
+    def kernel_profile(self, enable):
+        for r in self.rends:
+            r.kernel_profile(enable)
+
+    def kernel_times(self):
+        out = {}
+        for r in self.rends:
+            for k, (ms, n) in r.kernel_times().items():
+                a, b = out.get(k, (0.0, 0))
+                out[k] = (a + ms, b + n)
+        return out
+
+    def last_stats(self):
+        return self.rends[self.last].last_stats()
+
+
 class Session:
     """One workload on this rank: the scene in HBM and a `step()` that renders one frame (frames mode /
-    one part) or this rank's tile of one frame plus the pipelined gather (tiles mode)."""
+    one part) or this rank's tile of one frame plus the pipelined gather (tiles mode).
 
-    def __init__(self, R, workload, dev, local, rank, world, tiles, distributed, rend, gather="abi"):
+    in_flight (one part): consecutive frames alternate over that many render contexts (scene copy +
+    workspace each) on as many streams, each into its own output buffer, so frame k+1's waves fill the GPU
+    while frame k's last waves finish — how a renderer serving a stream of frames uses the library (the
+    multi-GPU group does the same per part).  Every step still renders one whole frame."""
+
+    def __init__(self, R, workload, dev, local, rank, world, tiles, distributed, rend, gather="abi", in_flight=1):
         import torch
         from rray_amd import dist as rdist
 
@@ -179,12 +210,22 @@ class Session:
         self.frame_t = None
         part, nparts = (rank, world) if tiles else (0, 1)
         rows = R.part_rows(self.H, part, nparts, BLOCK)
+        self.k = 0
+        self.slots = None
         if not self.multi:
             # the AA-averaged f64 image (the drop-in's Canvas, before `as u8`)
             self.tile = torch.zeros((len(rows), self.W, 3), dtype=torch.float64, device=dev)
             self.opts = R._lib.RenderOpts(self.aa, self.depth, 0, 0, part, nparts, BLOCK,
                                           R._lib.RR_OUT_AVG | R._lib.RR_NO_FRAME_TIMING)
             self.stream = torch.cuda.current_stream(dev)
+            if in_flight > 1:
+                extra = [R.Renderer(local) for _ in range(in_flight - 1)]
+                for r in extra:
+                    r.upload(self.scene)
+                self.slots = [(r, torch.cuda.Stream(dev), self.tile if i == 0 else torch.zeros_like(self.tile))
+                              for i, r in enumerate([rend] + extra)]
+                self.extra = extra
+                self.rend = Contexts([rend] + extra)
         elif gather == "abi":
             # the library's group context splits the frame into this rank's row tile, gathers the f64
             # tiles to rank 0 with one RCCL gather (double-buffered: frame k+1 renders while frame k is
@@ -206,6 +247,13 @@ class Session:
         import torch
 
         if not self.multi:
+            if self.slots:
+                j = self.k % len(self.slots)
+                r, st, out = self.slots[j]
+                r.render_device(self.cam, self.opts, None, out.data_ptr(), st.cuda_stream)
+                self.rend.last = j
+                self.k += 1
+                return
             self.rend.render_device(self.cam, self.opts, None, self.tile.data_ptr(), self.stream.cuda_stream)
             return
         if self.gather == "abi":
@@ -226,7 +274,13 @@ class Session:
             return self.frame_t.cpu().numpy() if self.frame_t is not None else None
         if self.multi:
             return self.pipe.frame.cpu().numpy() if self.pipe.frame is not None else None
+        if self.slots:
+            return self.slots[(self.k - 1) % len(self.slots)][2].cpu().numpy()
         return self.tile.cpu().numpy()
+
+    def close(self):
+        for r in getattr(self, "extra", []):
+            r.close()
 
 
 def timed_loop(sess, steps, warmup, distributed, dist, torch, kernel_events="separate"):
@@ -462,7 +516,8 @@ def gpu_bench(args, world, mode, workload):
         rend = R.Renderer.rank(local, world, rank, uid[0])
     else:
         rend = R.Renderer(local)
-    sess = Session(R, workload, dev, local, rank, world, tiles, distributed, rend, args.gather)
+    in_flight = max(1, args.in_flight)
+    sess = Session(R, workload, dev, local, rank, world, tiles, distributed, rend, args.gather, in_flight)
     big = WORKLOADS[workload][1] * WORKLOADS[workload][2] * WORKLOADS[workload][3] ** 2 > 20_000_000
     steps = args.steps if args.steps is not None else (10 if big else 50)
     warmup = args.warmup if args.warmup is not None else (2 if big else 10)
@@ -485,16 +540,24 @@ def gpu_bench(args, world, mode, workload):
             full = one.render(sess.cam, aa=sess.aa, max_depth=sess.depth)["avg"]
             identity = {"bit_identical_to_1_part": bool(np.array_equal(gathered, full)),
                         "max_abs_diff": float(np.max(np.abs(gathered - full)))}
-            a = Session(R, workload, dev, local, 0, 1, True, False, one)
+            a = Session(R, workload, dev, local, 0, 1, True, False, one, in_flight=in_flight)
             k1 = max(2, min(steps, 5))
             a_el, _, _, _, _ = timed_loop(a, k1, 1, False, dist, torch)
             single = {"n_gpus": 1, "steps": k1, "ms_per_step": round(a_el / k1 * 1e3, 4),
-                      "value": round(a.W * a.H * a.aa * a.aa * k1 / a_el / 1e6, 3),
+                      "value": round(a.W * a.H * a.aa * a.aa * k1 / a_el / 1e6, 3), "frames_in_flight": in_flight,
                       "note": "the same frame rendered as one part on rank 0's GPU after the timed region"}
+            a.close()
             one.close()
         dist.barrier()
 
-    cpu = parity = anchor = cold = None
+    cpu = parity = anchor = cold = serial = None
+    if rank == 0 and world == 1 and not args.force_dist and sess.slots:
+        # the same frames one at a time (one context, one stream): the per-frame latency a single render sees
+        ser = Session(R, workload, dev, local, 0, 1, tiles, False, rend)
+        s_el, _, s_kt, _, _ = timed_loop(ser, steps, warmup, False, dist, torch)
+        serial = {"frames_in_flight": 1, "steps": steps, "ms_per_step": round(s_el / steps * 1e3, 4),
+                  "value": round(samples_per_frame * steps / s_el / 1e6, 3),
+                  "kernels_ms_per_step": {k: round(v[0] / steps, 4) for k, v in s_kt.items() if v[1]}}
     if rank == 0 and world == 1 and not args.force_dist and not args.no_cold:
         cold = [cold_frames(R, w, dev, local, torch) for w in dict.fromkeys([workload, "c4_teapot"])]
     if rank == 0 and world == 1 and not args.force_dist:
@@ -502,11 +565,12 @@ def gpu_bench(args, world, mode, workload):
             cpu, parity = cpu_leg(sess, args, sess.frame())
         if not args.no_anchor and workload != MULTI_GPU_WORKLOAD:
             # the N = 1 point of the multi-GPU curve: C3 as one part on this GPU
-            a = Session(R, MULTI_GPU_WORKLOAD, dev, local, 0, 1, True, False, rend)
+            a = Session(R, MULTI_GPU_WORKLOAD, dev, local, 0, 1, True, False, rend, in_flight=in_flight)
             a_el, _, _, _, _ = timed_loop(a, 5, 1, False, dist, torch)
+            a.close()
             a_samples = a.W * a.H * a.aa * a.aa
             anchor = {"workload": MULTI_GPU_WORKLOAD, "n_gpus": 1, "value": round(a_samples * 5 / a_el / 1e6, 3),
-                      "ms_per_step": round(a_el / 5 * 1e3, 4), "steps": 5, "warmup": 1,
+                      "ms_per_step": round(a_el / 5 * 1e3, 4), "steps": 5, "warmup": 1, "frames_in_flight": in_flight,
                       "note": "N=1 value of the N>1 workload (row tiles with nparts=1), for the scaling curve"}
     if rank == 0:
         via = ("library RCCL group: rr_create_rank + rr_render_gather_device" if args.gather == "abi" else
@@ -525,6 +589,8 @@ def gpu_bench(args, world, mode, workload):
                            "parallelism": par},
                 "roofline": roofline, "cpu_baseline": cpu, "parity_sample": parity, "cold_frames": cold,
                 "build": {"library_digest": lib_digest, "source_digest": src_digest, "match": lib_digest == src_digest},
+                "frames_in_flight": 2 if sess.multi and args.gather == "abi" else len(sess.slots or [0]),
+                "serial": serial,
                 "tile_identity": identity, "scaling_anchor": anchor, "single_gpu": single,
                 "speedup_vs_single_gpu": round(value / single["value"], 3) if single else None,
                 "kernels_ms_per_step": {k: round(v[0] / steps, 4) for k, v in ktimes.items() if v[1]},
@@ -535,6 +601,7 @@ def gpu_bench(args, world, mode, workload):
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+    sess.close()
     rend.close()
 
 

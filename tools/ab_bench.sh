@@ -11,5 +11,5 @@ for spec in "$@"; do
     timeout -k 10 200 python bench.py ${BENCH_ARGS:---steps 20 --warmup 3} > gpurun_out/ab_$label.log 2>&1 ) || { echo "$label failed"; tail -5 gpurun_out/ab_$label.log; exit 1; }
   tail -1 gpurun_out/ab_$label.log | python -c "
 import json,sys; d=json.loads(sys.stdin.read())
-print('$label', d['value'], 'ms/step', d['ms_per_step'], 'kernels', d['kernels_ms_per_step'], 'parity', d.get('parity_sample'))"
+print('$label', d['value'], 'ms/step', d['ms_per_step'], 'serial', (d.get('serial') or {}).get('ms_per_step'), 'kernels', d['kernels_ms_per_step'], 'parity', d.get('parity_sample'))"
 done

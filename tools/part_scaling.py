@@ -1,10 +1,10 @@
 """Strong-scaling predictor on one GPU: the C3 frame split into N row-tile parts
 (the partition bench.py --gpus N uses), each part rendered alone on this GPU, K frames timed with HIP
 events on the render stream.  The slowest part's time is what one rank of an N-GPU run spends per
-frame before the gather, so 1-part time / max part time bounds the N-GPU speedup from above (the
-gather and the root's un-interleave come on top, overlapped with the next frame's render).  Also
-the virtual group (rr_create_virtual: the N parts, their padded tiles, the device-local stand-in for
-the RCCL gather and the un-interleave) per frame, all parts on this one GPU.
+frame before the transfer, so 1-part time / max part time bounds the N-GPU speedup from above (the
+transfer of the runs to rank 0 comes on top, overlapped with the next frame's render).  Each part renders
+in one render context here.  Also the virtual group (rr_create_virtual: the N parts, their tiles, the
+device-local stand-in for the RCCL transfer) per frame, all parts on this one GPU.
 Usage: python tools/part_scaling.py [workload] [steps] [part P N]   ->  JSON on stdout.
 """
 import json
