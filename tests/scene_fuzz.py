@@ -100,6 +100,12 @@ class Pair:
         self.o.point_light(pos, color)
         self.log.append(f"point light {pos}")
 
+    def area_light(self, corner, u, v, level, color=(1.0, 1.0, 1.0)):
+        corner, u, v = (tuple(float(x) for x in a) for a in (corner, u, v))
+        self.b.area_light(corner, u, v, color, int(level))
+        self.o.area_light(corner, u, v, color, int(level))
+        self.log.append(f"area light corner={corner} u={u} v={v} level={level}")
+
 
 def _mul(M, *ts):
     """ts applied first to last (the YAML transform list order, scene_builder_yaml.rs:218-224)."""
@@ -282,6 +288,58 @@ def build(seed):
         up = (1.0, 0.0, 0.0)
     P.log.append(f"camera from={frm} to={to} up={up} fov={fov} depth={depth}")
     return P, {"from_": tuple(float(x) for x in frm), "to": tuple(float(x) for x in to), "up": up, "fov": fov}, depth, cat
+
+
+def build_area(seed):
+    """Area-light scenes for the light-hull pre-test (render_levels.inc area_may_shadow): occluders placed just
+    inside and just outside the capsule around the segment from a floor point to the light's centre, tilted and
+    light-side planes, skewed / tiny / huge light parallelograms, groups and cubes.  -> (Pair, camera spec, depth,
+    category)."""
+    rng = np.random.default_rng(20_000 + seed)
+    P = Pair()
+    M = P.M
+    kind = seed % 4
+    # the light: a parallelogram above the scene (sometimes skewed, tiny or huge), a few cells per side
+    size = [0.3, 1.5, 6.0, 1e-3][int(rng.integers(4))]
+    corner = np.array([rng.uniform(-6, 6), rng.uniform(4, 9), rng.uniform(-8, 2)])
+    u = np.array([1.0, 0.0, 0.0]) * size
+    v = (np.array([0.0, 1.0, 0.0]) if rng.random() < 0.5 else _unit(rng)) * size * rng.uniform(0.3, 1.5)
+    if rng.random() < 0.4:
+        u = _unit(rng) * size
+    level = int(rng.integers(1, 5))
+    P.area_light(corner, u, v, level)
+    qc = corner + 0.5 * u + 0.5 * v
+    qr = 0.5 * max(np.linalg.norm(u + v), np.linalg.norm(u - v))
+    # the floor, tilted at times; a second plane near the light's side at times
+    tilt = float(rng.uniform(-0.3, 0.3)) if rng.random() < 0.4 else 0.0
+    P.obj("plane", _mul(M, M.rotate("z", tilt)), _material(rng, reflective_p=0.5), _color(rng))
+    if kind == 1:  # a wall the light's hull straddles or just misses
+        P.obj("plane", _mul(M, M.rotate("x", math.pi / 2), M.translate(0.0, 0.0, float(corner[2] + rng.uniform(-0.5, 0.5)))),
+              _material(rng), _color(rng))
+    parent = -1
+    if kind == 2:
+        parent = P.obj("group", _mul(M, M.scale(*rng.uniform(0.5, 2.0, 3)), M.translate(*rng.uniform(-1, 1, 3))))
+    for _ in range(int(rng.integers(2, 9))):
+        # a floor point in view, the segment to the light centre, an occluder at distance ~ r + qr from it
+        fp = np.array([rng.uniform(-3, 3), 0.0, rng.uniform(-1, 5)])
+        t = rng.uniform(0.1, 0.9)
+        a = fp + t * (qc - fp)
+        r = _logu(rng, 0.05, 1.0)
+        off = (r + qr * t) * (1.0 + float(rng.choice([-1e-3, 1e-6, 1e-3, 0.05, -0.05])))
+        c = a + _unit(rng) * off
+        if kind == 3 and rng.random() < 0.5:
+            tr = _mul(M, M.scale(r, r, r), _rot(M, rng), M.translate(*[float(x) for x in c]))
+            P.obj("cube", tr, _material(rng, reflective_p=0.5), _color(rng), parent=parent)
+        else:
+            P.obj("sphere", _mul(M, M.scale(r, r, r), M.translate(*[float(x) for x in c])),
+                  _material(rng, reflective_p=0.5), _color(rng), parent)
+    if rng.random() < 0.3:
+        P.light(qc + rng.uniform(-2, 2, 3))
+    frm = (float(rng.uniform(-2, 2)), float(rng.uniform(1.5, 4)), -6.0)
+    to = (0.0, 0.5, 2.0)
+    fov = float(rng.uniform(0.8, 1.2))
+    P.log.append(f"camera from={frm} to={to} fov={fov} depth=3")
+    return P, {"from_": frm, "to": to, "up": (0.0, 1.0, 0.0), "fov": fov}, 3, f"area{kind}"
 
 
 def cameras(P, spec, W, H):

@@ -35,3 +35,22 @@ def test_fuzz_scene_builds_identically(oracle_mod, seed):
     assert time.perf_counter() - t < 30
     print(f"seed {seed} {cat}: {n} objects, rays {st['rays']}, shade {st['shade_events']}, "
           f"lit px {float(np.mean(canvas.sum(axis=2) > 0)):.2f}")
+
+
+@pytest.mark.parametrize("seed", range(32))
+def test_area_fuzz_scene_builds_identically(oracle_mod, seed):
+    """The area-light fuzz scenes (scene_fuzz.build_area) hold the same inverses on both sides and render to
+    finite values with some light and some shadow."""
+    import rray_amd as R
+
+    P, spec, depth, cat = F.build_area(seed)
+    desc = P.b.desc()
+    n = desc.n_objects
+    inv = np.zeros((n, 16))
+    R._lib.check(R.lib().rr_scene_inspect(C.byref(desc), inv.ctypes.data_as(R._lib._D), None, None))
+    for bid, oid in P.ids.items():
+        assert np.array_equal(inv[bid], np.array(P.o.inverse_of(oid))), (seed, cat, bid)
+    cam, ocam = F.cameras(P, spec, 24, 16)
+    canvas, st = P.o.render(ocam, max_depth=depth, seed=seed)
+    assert np.isfinite(canvas).all(), (seed, cat)
+    assert st["shadow_rays"] > 0, (seed, cat)

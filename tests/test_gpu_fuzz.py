@@ -63,3 +63,30 @@ def test_fuzz_scene_bit_exact(renderer, seed):
         print(f"seed {seed} ({cat}): {len(pow_only)} samples differ from libm pow by its rounding only")
     assert ok, f"seed {seed} ({cat})"
     assert float(np.max(np.abs(got["avg"] - P.o.aa_average(canvas, aa)))) <= 1e-12
+
+
+@pytest.mark.parametrize("seed", range(32))
+def test_area_light_fuzz_bit_exact(renderer, seed):
+    """Area lights (light.rs:47-96) with occluders at the edge of the light-hull pre-test's capsule
+    (render_levels.inc area_may_shadow: events whose hull no node reaches skip their level^2 walks): the
+    canvas must equal the oracle's (correctly rounded powers) bit for bit, with the same ray counts."""
+    P, spec, depth, cat = F.build_area(seed)
+    aa = 2 if seed % 2 else 1
+    W, H = (24, 16) if aa == 2 else (40, 24)
+    cam, ocam = F.cameras(P, spec, W * aa, H * aa)
+    renderer.upload(P.b)
+    got = renderer.render(cam, aa=aa, max_depth=depth, seed=seed, canvas=True)
+    P.o.set_pow_mode(1)
+    canvas_cr, st = P.o.render(ocam, max_depth=depth, seed=seed)
+    P.o.set_pow_mode(0)
+    diff = np.argwhere((got["canvas"] != canvas_cr).any(axis=2))
+    counts = {k: (got["stats"][k], v) for k, v in (("rays", st["rays"] - st["shadow_rays"]),
+                                                    ("shadow_rays", st["shadow_rays"]),
+                                                    ("shade_events", st["shade_events"]))}
+    ok = len(diff) == 0 and all(a == b for a, b in counts.values())
+    if not ok:
+        print(f"seed {seed} ({cat}) {W}x{H} aa{aa}: {len(diff)} samples differ; counts (gpu, oracle) {counts}")
+        for y, x in diff[:10]:
+            print(f"  sample ({x},{y}): gpu {got['canvas'][y, x].tolist()} oracle {canvas_cr[y, x].tolist()}")
+        print("\n".join(P.log))
+    assert ok, f"seed {seed} ({cat})"
