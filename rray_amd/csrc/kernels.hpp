@@ -49,6 +49,7 @@ struct LevelArgs {
     // cycles (or null).  The order changes only which wave renders which tile, never a result.
     const uint32_t* tile_perm;
     uint32_t* tile_cost;
+    int32_t order_group;     // tile_perm's units: 1 (one wave's tile each) or 4 (a block's four tiles)
     int32_t pad_children;    // fused levels: children in per-wave 64-slot blocks (holes: Event.parent == -2)
     // chain kernels (chain_kernel): the deep queue (segmented like the fused levels' queues: the camera launch
     // appends to seg_out_count / seg_cap_out, the deep launch reads seg_count / seg_cap) and the depth at which
@@ -148,7 +149,11 @@ hipError_t launch_pixel_wave_bundles(const LevelArgs& A, float* out, int64_t n_w
 hipError_t launch_tile_guess(const DevScene& S, const float* bundles, uint32_t* cost, int64_t n_tiles, hipStream_t stream);
 // perm = tiles by decreasing recorded cost (LevelArgs.tile_cost), for the next frames' level-0 launches;
 // scratch = 256 u32 of device memory (bucket counters)
-hipError_t launch_tile_order(const uint32_t* cost, uint32_t* perm, uint32_t* scratch, int64_t n_tiles, hipStream_t stream);
+constexpr int RR_ORDER_GROUP = 4;
+// group: the sort's unit, 1 tile or RR_ORDER_GROUP consecutive tiles (one launch block's waves; perm then maps a launch
+// block to a tile group)
+hipError_t launch_tile_order(const uint32_t* cost, uint32_t* perm, uint32_t* scratch, int64_t n_tiles, int group,
+                             hipStream_t stream);
 // trace + shade run as one kernel per level (no transparent material, so no n1/n2 walk between them);
 // those levels finish their reflection chains themselves and need no combine pass
 bool fused_levels(const DevScene& S);

@@ -198,24 +198,24 @@ __device__ __forceinline__ int cost_bucket(uint32_t c) {
     return 255 - (q > 255 ? 255 : q);
 }
 constexpr int RR_ORDER_BLOCK = 256, RR_ORDER_PER_THREAD = 16;  // 4096 tiles per block
-// the launch blocks' units: groups of RR_ORDER_GROUP consecutive tiles (a block's four waves), whose cost is the
-// sum of their tiles' (saturating)
-constexpr int RR_ORDER_GROUP = 4;
-__device__ __forceinline__ uint32_t group_cost(const uint32_t* cost, int64_t g) {
+// the sort's units: single tiles (group 1) or groups of RR_ORDER_GROUP consecutive tiles (a block's four waves),
+// whose cost is the sum of their tiles' (saturating)
+__device__ __forceinline__ uint32_t group_cost(const uint32_t* cost, int64_t g, int group) {
+    if (group == 1) return cost[g];
     uint64_t c = 0;
 #pragma unroll
     for (int k = 0; k < RR_ORDER_GROUP; ++k) c += cost[g * RR_ORDER_GROUP + k];
     return c > 0xffffffffull ? 0xffffffffu : (uint32_t)c;
 }
 __global__ void __launch_bounds__(RR_ORDER_BLOCK) tile_hist_kernel(const uint32_t* __restrict__ cost,
-                                                                   uint32_t* __restrict__ hist, int64_t n) {
+                                                                   uint32_t* __restrict__ hist, int64_t n, int group) {
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
     const int64_t b0 = (int64_t)blockIdx.x * RR_ORDER_BLOCK * RR_ORDER_PER_THREAD;
     for (int k = 0; k < RR_ORDER_PER_THREAD; ++k) {
         const int64_t i = b0 + (int64_t)k * RR_ORDER_BLOCK + threadIdx.x;
-        if (i < n) atomicAdd(&h[cost_bucket(group_cost(cost, i))], 1u);
+        if (i < n) atomicAdd(&h[cost_bucket(group_cost(cost, i, group))], 1u);
     }
     __syncthreads();
     if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
@@ -236,7 +236,7 @@ __global__ void __launch_bounds__(256) tile_scan_kernel(uint32_t* __restrict__ h
 }
 __global__ void __launch_bounds__(RR_ORDER_BLOCK) tile_scatter_kernel(const uint32_t* __restrict__ cost,
                                                                       uint32_t* __restrict__ cursor,
-                                                                      uint32_t* __restrict__ perm, int64_t n) {
+                                                                      uint32_t* __restrict__ perm, int64_t n, int group) {
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
@@ -245,7 +245,7 @@ __global__ void __launch_bounds__(RR_ORDER_BLOCK) tile_scatter_kernel(const uint
 #pragma unroll
     for (int k = 0; k < RR_ORDER_PER_THREAD; ++k) {
         const int64_t i = b0 + (int64_t)k * RR_ORDER_BLOCK + threadIdx.x;
-        bk[k] = i < n ? cost_bucket(group_cost(cost, i)) : -1;
+        bk[k] = i < n ? cost_bucket(group_cost(cost, i, group)) : -1;
         if (bk[k] >= 0) atomicAdd(&h[bk[k]], 1u);
     }
     __syncthreads();
@@ -261,17 +261,19 @@ __global__ void __launch_bounds__(RR_ORDER_BLOCK) tile_scatter_kernel(const uint
     }
 }
 
-// scratch: 256 u32 of device memory for the bucket counters; perm: launch block -> tile group (n_tiles a multiple of
-// RR_ORDER_GROUP)
-hipError_t launch_tile_order(const uint32_t* cost, uint32_t* perm, uint32_t* scratch, int64_t n_tiles, hipStream_t st) {
+// scratch: 256 u32 of device memory for the bucket counters; perm: launch slot -> tile (group 1) or launch block ->
+// tile group (group RR_ORDER_GROUP; n_tiles a multiple of it)
+hipError_t launch_tile_order(const uint32_t* cost, uint32_t* perm, uint32_t* scratch, int64_t n_tiles, int group,
+                             hipStream_t st) {
     if (n_tiles <= 0) return hipSuccess;
-    n_tiles /= RR_ORDER_GROUP;  // the sort's units: tile groups
+    if (group != 1 && group != RR_ORDER_GROUP) return hipErrorInvalidValue;
+    n_tiles /= group;  // the sort's units: tiles or tile groups
     const unsigned blocks = (unsigned)((n_tiles + RR_ORDER_BLOCK * RR_ORDER_PER_THREAD - 1) / (RR_ORDER_BLOCK * RR_ORDER_PER_THREAD));
     hipError_t e = hipMemsetAsync(scratch, 0, 256 * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(tile_hist_kernel, dim3(blocks), dim3(RR_ORDER_BLOCK), 0, st, cost, scratch, n_tiles);
+    hipLaunchKernelGGL(tile_hist_kernel, dim3(blocks), dim3(RR_ORDER_BLOCK), 0, st, cost, scratch, n_tiles, group);
     hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(256), 0, st, scratch);
-    hipLaunchKernelGGL(tile_scatter_kernel, dim3(blocks), dim3(RR_ORDER_BLOCK), 0, st, cost, scratch, perm, n_tiles);
+    hipLaunchKernelGGL(tile_scatter_kernel, dim3(blocks), dim3(RR_ORDER_BLOCK), 0, st, cost, scratch, perm, n_tiles, group);
     return hipGetLastError();
 }
 

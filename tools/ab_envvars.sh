@@ -16,7 +16,7 @@ for rep in ${REPS:-1 2}; do
   for wl in ${WLS:-c2_s1024}; do
     for e in "${envs[@]}"; do
       env $e timeout -k 10 300 python bench.py --workload "$wl" --steps "${STEPS:-30}" --warmup 5 --no-cpu-baseline \
-        --no-anchor > gpurun_out/ab_run.log 2>&1 || { echo "bench failed: $wl [$e]"; tail -5 gpurun_out/ab_run.log; exit 1; }
+        --no-anchor ${BENCH_ARGS:-} > gpurun_out/ab_run.log 2>&1 || { echo "bench failed: $wl [$e]"; tail -5 gpurun_out/ab_run.log; exit 1; }
       python - "$wl" "$e" <<'PY'
 import json, sys
 d = json.loads([l for l in open("gpurun_out/ab_run.log") if l.startswith("{")][-1])

@@ -16,7 +16,7 @@ run() {  # name, timeout, rocprof args...  (PSTEPS: steps of this pass)
   local name=$1 t=$2; shift 2
   echo "== $name ($(date +%T))"
   (cd /tmp && timeout -k 10 "$t" rocprofv3 "$@" -d "$OUT/$name" -o run --output-format csv -- \
-      python3 "$ROOTDIR/bench.py" --workload "$WL" --steps "${PSTEPS:-5}" --warmup "${PWARM:-1}" --no-cpu-baseline --no-anchor) > "$OUT/$name.log" 2>&1
+      python3 "$ROOTDIR/bench.py" --workload "$WL" --steps "${PSTEPS:-5}" --warmup "${PWARM:-1}" --no-cpu-baseline --no-anchor --no-cold --in-flight 1) > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "== $name rc=$rc"; tail -n 3 "$OUT/$name.log"
   return $rc
