@@ -176,9 +176,9 @@ def test_shape_scenes(renderer, name, W, H, aa):
     canvas, st = o.render(cam, max_depth=5)
     _compare(got["canvas"], canvas, name + " canvas")
     _, exact = _compare(got["avg"], o.aa_average(canvas, aa), name + " avg")
-    # regression guard on the bit-exact fraction: torus hits carry OCML's last-ulp transcendentals (DESIGN.md
-    # §3.8: 0.87-0.93 of the averaged channels measured); elsewhere only libm pow's last ulp differs
-    assert exact >= (0.85 if "torus" in name else 0.999), f"{name}: bit-exact fraction {exact:.6f}"
+    # regression guard on the bit-exact fraction: only libm's last ulp may differ (pow; the torus solver's
+    # transcendentals round like glibc since round 4, DESIGN.md §3.8 — measured 1.000000 on both torus cases)
+    assert exact >= 0.999, f"{name}: bit-exact fraction {exact:.6f}"
     assert got["stats"]["rays"] == st["rays"] - st["shadow_rays"]
     assert got["stats"]["shadow_rays"] == st["shadow_rays"]
     assert got["stats"]["shade_events"] == st["shade_events"]
@@ -335,9 +335,10 @@ def test_pixel_waves_odd_sizes(R, renderer, W, H):
 def test_torus_jpeg_texture_scene(renderer, W, H, aa):
     """The reference's examples/objects/torus.yaml: a torus with the JPEG texture
     examples/Texturelabs_Stone_138M.jpg (texture.rs:15-19), decoded by the product front-end
-    (jpeg.cpp) and by PIL in the oracle.  The texels are bit-identical (tests/test_jpeg.py); the torus
-    hits carry OCML's last-ulp acos / cos / cbrt, so the images are held to the
-    north_star tolerance like `shapes_torus.yaml`, with equal recursion counters."""
+    (jpeg.cpp) and by PIL in the oracle.  The texels are bit-identical (tests/test_jpeg.py), and the torus
+    solver's transcendentals round like the host glibc (host_libm.inc), so the frames are
+    bit-exact (measured 1.000000, round 4); held to the north_star tolerance like every scene, with equal
+    recursion counters."""
     root = os.path.join(GOLDEN, "example1")
     scene, (o, cam) = _yaml_pair("torus.yaml", W, H, aa, obj_root=root, path=os.path.join(root, "torus.yaml"))
     renderer.upload(scene)
@@ -345,8 +346,8 @@ def test_torus_jpeg_texture_scene(renderer, W, H, aa):
     canvas, st = o.render(cam, max_depth=5)
     _, exact_c = _compare(got["canvas"], canvas, "torus.yaml canvas")
     _, exact = _compare(got["avg"], o.aa_average(canvas, aa), "torus.yaml avg")
-    # regression guard (OCML's last ulp in the torus hits; measured 0.969 / 0.934 at 160x80 aa2)
-    assert exact_c >= 0.95 and exact >= 0.9, f"torus.yaml: bit-exact fractions {exact_c:.4f} / {exact:.4f}"
+    # regression guard: glibc-rounded transcendentals leave at most glibc's rare last-ulp misses
+    assert exact_c >= 0.999 and exact >= 0.999, f"torus.yaml: bit-exact fractions {exact_c:.4f} / {exact:.4f}"
     assert got["stats"]["rays"] == st["rays"] - st["shadow_rays"]
     assert got["stats"]["shade_events"] == st["shade_events"]
 
