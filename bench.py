@@ -122,9 +122,10 @@ def main():
                     help="CPU sample: one 8-row band in every STRIDE bands (default sized to ~10-30 s)")
     ap.add_argument("--no-anchor", action="store_true", help="N=1: skip the C3 scaling anchor")
     ap.add_argument("--no-cold", action="store_true", help="N=1: skip the cold-frame measurements")
-    ap.add_argument("--in-flight", type=int, default=2,
+    ap.add_argument("--in-flight", type=int, default=1,
                     help="whole-frame steps: frames alternate over this many render contexts and streams (1 = "
-                         "one frame at a time; N=1 lines with more also time 1 as `serial`)")
+                         "one frame at a time, the default: two measured no faster on C2 or C3, "
+                         "profiles/r04/pipe_probe.txt; N=1 lines with more also time 1 as `serial`)")
     ap.add_argument("--max-depth", type=int, default=None,
                     help="experiment: override the workload's recursion depth (the line then names it in config)")
     ap.add_argument("--kernel-events", choices=("separate", "timed"), default="separate",

@@ -105,6 +105,10 @@ def main():
         opts = R._lib.RenderOpts(aa, depth, 0, 0, 0, 1, bench.BLOCK, flags)
         for _ in range(2):
             g.render_gather_device(scene.camera, opts, frame.data_ptr(), st.cuda_stream)
+        # the group's renders run on its own streams and wait only for the transfer that last read their tile
+        # buffer, not for the caller's stream: drain the warm-up frames first, or the first timed frame's render
+        # overlaps them and escapes the events (the round-4 5.16 ms "virtual_group_1" against 6.32 ms per part)
+        torch.cuda.synchronize(dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
         for _ in range(steps):
