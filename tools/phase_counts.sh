@@ -13,7 +13,7 @@ for k in ${KS:-1 2 3 4 5 0}; do
   mkdir -p "$OUT"
   (cd /tmp && RRAY_PHASE_EXIT=$k timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM \
      SQ_INSTS_VMEM_RD SQ_INSTS_LDS -d "$OUT" -o run --output-format csv -- \
-     python3 "$ROOTDIR/bench.py" --workload "$WL" --steps 3 --warmup 1 --no-cpu-baseline --no-anchor) > "$OUT.log" 2>&1 || {
+     python3 "$ROOTDIR/bench.py" --workload "$WL" --steps 3 --warmup 1 --no-cpu-baseline --no-anchor --no-cold) > "$OUT.log" 2>&1 || {
      echo "k=$k failed"; tail -5 "$OUT.log"; exit 1; }
 done
 python3 - "$WL" <<'PY'
