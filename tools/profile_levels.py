@@ -20,13 +20,16 @@ def short(name):
 
 def frames(rows, key):
     """Label each rr:: dispatch with (short name, occurrence index inside its frame).  A frame starts at
-    each dispatch of the first rr:: kernel seen (other than the once-per-camera tile_bundle_kernel)."""
+    each dispatch of the first rr:: kernel seen other than the kernels that run once per camera or layout (the
+    camera bundles, the first frame's tile-order guess) or every few frames (the tile-order sort)."""
+    occasional = {"tile_bundle_kernel", "pixel_wave_bundle_kernel", "tile_guess_kernel", "tile_hist_kernel",
+                  "tile_scan_kernel", "tile_scatter_kernel"}
     out, first, seen = [], None, collections.Counter()
     for r in rows:
         k = short(r["Kernel_Name"])
         if not k:
             continue
-        if first is None and k != "tile_bundle_kernel":  # bundles: once per camera, not per frame
+        if first is None and k not in occasional:  # once per camera / layout, not per frame
             first = k
         if k == first:
             seen = collections.Counter()
