@@ -3,6 +3,7 @@ tiles gathered back to back (multi.cpp's ncclGather layout) and the library's un
 (rr_unshuffle_host, the index arithmetic of multi.cpp's device kernel) reassemble a frame bit-identical
 to the single-process render, in f64 like the product's tiles.  The tiles are rendered by the oracle here
 (test stand-in for the GPU; the GPU tests test_virtual_group_* run the same assembly on the device)."""
+import datetime
 import os
 import socket
 
@@ -32,7 +33,8 @@ def _worker(rank, world, port, W, H, block, q):
     from rray_amd import dist as rdist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a bounded rendezvous: a port lost to another process fails the test in seconds, not after the 30-min default
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
     text = open(os.path.join(ROOT, "scenes", "c3_s1024_reflect.yaml")).read()
     o, cam = build_from_yaml(text, W, H, 1)
     canvas, _ = o.render(cam, max_depth=5, threads=2, band=block, band_stride=world, band_phase=rank)
@@ -56,7 +58,8 @@ def _pipe_worker(rank, world, port, W, H, block, q):
     from rray_amd import dist as rdist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a bounded rendezvous: a port lost to another process fails the test in seconds, not after the 30-min default
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
     text = open(os.path.join(ROOT, "scenes", "c3_s1024_reflect.yaml")).read()
     o, cam = build_from_yaml(text, W, H, 1)
     canvas, _ = o.render(cam, max_depth=5, threads=2, band=block, band_stride=world, band_phase=rank)
