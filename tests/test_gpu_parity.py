@@ -111,6 +111,31 @@ def test_cost_ordered_tiles_change_no_result(R, renderer):
     assert np.array_equal(back["avg"], first["avg"])
 
 
+@pytest.mark.parametrize("name,W,H,aa", [("c4_teapot.yaml", 64, 40, 2), ("c3_s1024_reflect.yaml", 48, 24, 3)])
+def test_order_units_change_no_result(renderer, monkeypatch, name, W, H, aa):
+    """The cost order's unit (api.cpp run_levels) — one camera wave (the default) or a block's four adjacent tiles
+    (RRAY_ORDER_GROUP=4) — changes which wave renders which tile, never a pixel: a group scene's level-0 frames and
+    a chain scene's pixel-wave frames (aa 3), three under each unit (guessed order, then measured orders), are
+    bit-identical to each other and within the gate of the oracle, counters equal."""
+    scene, (o, cam) = _yaml_pair(name, W, H, aa)
+    renderer.upload(scene)
+    canvas, _ = o.render(cam, max_depth=5)
+    ref = o.aa_average(canvas, aa)
+    first = None
+    drop = ("kernel_ms",)  # timing, not a count
+    for unit in ("1", "4"):
+        monkeypatch.setenv("RRAY_ORDER_GROUP", unit)
+        for k in range(3):
+            got = renderer.render(scene.camera, aa=aa, max_depth=5)
+            if first is None:
+                _compare(got["avg"], ref, f"{name} {W}x{H} aa{aa} order unit {unit}")
+                first = got
+                continue
+            assert np.array_equal(got["avg"], first["avg"]), f"order unit {unit}, frame {k + 1}"
+            assert {q: v for q, v in got["stats"].items() if q not in drop} == \
+                {q: v for q, v in first["stats"].items() if q not in drop}
+
+
 @pytest.mark.parametrize("name,W,H,aa", [("c4_teapot.yaml", 48, 28, 2), ("c4_teapot.yaml", 40, 24, 4),
                                          ("c2_s1024.yaml", 32, 20, 4), ("c2_s1024.yaml", 16, 10, 8),
                                          ("c1_readme.yaml", 24, 16, 2)])
