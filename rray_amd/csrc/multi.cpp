@@ -102,6 +102,7 @@ struct rr_group {
     hipEvent_t ev_caller = nullptr;       // root: the caller's stream position at the gather call
     std::vector<DevMem> tile[2];          // per local part: its tile (rows of the part, in tile order)
     DevMem frame;                         // root: assembled frame for the blocking rr_render
+    DevMem stage;                         // root of an RCCL group: every part's tile, received back to back
     int64_t k = 0;                        // frames issued (buffer and render context = k % 2)
     int nlocal() const { return (int)devices.size(); }
     int last() const { return k > 0 ? (int)((k - 1) & 1) : 0; }  // the set that rendered the latest frame
@@ -251,6 +252,7 @@ void group_destroy(rr_group* g) {
         if (l < g->comm_st.size() && g->comm_st[l]) (void)hipStreamDestroy(g->comm_st[l]);
         if (l == 0 && g->root_here()) {
             g->frame.release();
+            g->stage.release();
             if (g->ev_caller) (void)hipEventDestroy(g->ev_caller);
         }
     }
@@ -302,6 +304,10 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
         GHIP(hipSetDevice(g->devices[l]));
         GHIP(g->tile[b][l].ensure((size_t)part_rows_count(H, so.part, g->nranks, block) * (size_t)row * sizeof(double)));
     }
+    if (g->root_here() && !g->virt) {  // the receive staging buffer (the whole frame's rows), before any work is enqueued
+        GHIP(hipSetDevice(g->devices[0]));
+        GHIP(g->stage.ensure((size_t)H * (size_t)row * sizeof(double)));
+    }
     if (g->root_here() && stream) {
         GHIP(hipSetDevice(g->devices[0]));
         GHIP(hipEventRecord(g->ev_caller, (hipStream_t)stream));
@@ -327,30 +333,41 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
             GHIP(launch_place_tile(static_cast<const double*>(g->tile[b][l].p), frame, W,
                                    part_rows_count(H, l, g->nranks, block), l, g->nranks, block, g->comm_st[0]));
     } else {
-        // one RCCL group per frame: each local part sends its runs to rank 0, and rank 0 receives every part's
-        // runs (its own from itself) into their frame rows.  Both sides enumerate the runs with
-        // for_each_part_run, so the operations between a pair of ranks pair up in order.  The group is always
-        // closed, also when posting an operation fails.
+        // one RCCL group per frame: each local part sends its whole tile to rank 0 in one ncclSend, and rank 0
+        // receives every part's tile (its own from itself) back to back into the staging buffer, then places each
+        // tile's rows into their frame rows with one copy kernel per part on the same stream (HBM-bound, ~2 x 199
+        // MB per C3 frame, overlapped with the next frame's render).  One operation per part: the round-4 first
+        // cut posted one send / receive per 8-row run (270 per C3 frame on rank 0), and the per-operation cost
+        // made the one-rank group's frame 1.49 ms slower than the single render (7.83 vs 6.34 ms).  The group is
+        // always closed, also when posting an operation fails.
+        double* stage = g->root_here() ? static_cast<double*>(g->stage.p) : nullptr;
         ncclResult_t r = ncclGroupStart();
         if (r == ncclSuccess) {
             for (int l = 0; l < n && r == ncclSuccess; ++l) {
-                const double* t = static_cast<const double*>(g->tile[b][l].p);
-                for_each_part_run(H, g->rank0 + l, g->nranks, block, [&](int64_t j, int64_t, int64_t rows) {
-                    if (r == ncclSuccess)
-                        r = ncclSend(t + j * row, (size_t)(rows * row), ncclFloat64, 0, g->comms[l], g->comm_st[l]);
-                });
+                const int64_t rows = part_rows_count(H, g->rank0 + l, g->nranks, block);
+                if (rows > 0)
+                    r = ncclSend(g->tile[b][l].p, (size_t)(rows * row), ncclFloat64, 0, g->comms[l], g->comm_st[l]);
                 if (!(g->root_here() && l == 0)) continue;
-                for (int32_t p = 0; p < g->nranks && r == ncclSuccess; ++p)
-                    for_each_part_run(H, p, g->nranks, block, [&](int64_t, int64_t y, int64_t rows) {
-                        if (r == ncclSuccess)
-                            r = ncclRecv(frame + y * row, (size_t)(rows * row), ncclFloat64, p, g->comms[0],
-                                         g->comm_st[0]);
-                    });
+                int64_t off = 0;
+                for (int32_t p = 0; p < g->nranks && r == ncclSuccess; ++p) {
+                    const int64_t pr = part_rows_count(H, p, g->nranks, block);
+                    if (pr > 0) r = ncclRecv(stage + off * row, (size_t)(pr * row), ncclFloat64, p, g->comms[0], g->comm_st[0]);
+                    off += pr;
+                }
             }
             const ncclResult_t e = ncclGroupEnd();
             if (r == ncclSuccess) r = e;
         }
         if (r != ncclSuccess) return gfail(RR_E_HIP, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
+        if (g->root_here()) {
+            GHIP(hipSetDevice(g->devices[0]));
+            int64_t off = 0;
+            for (int32_t p = 0; p < g->nranks; ++p) {
+                const int64_t pr = part_rows_count(H, p, g->nranks, block);
+                GHIP(launch_place_tile(stage + off * row, frame, W, pr, p, g->nranks, block, g->comm_st[0]));
+                off += pr;
+            }
+        }
     }
     for (int l = 0; l < n; ++l) {  // a virtual group's tiles are all read on comm_st[0]
         GHIP(hipSetDevice(g->devices[l]));

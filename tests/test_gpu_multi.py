@@ -87,9 +87,9 @@ def test_virtual_group_assembles_the_frame(R, single, nparts, block):
 
 @pytest.mark.parametrize("block", [1, 3, 8])
 def test_rccl_group_receives_runs_in_frame_order(R, single, block):
-    """The 1-device RCCL group at several block sizes: 40 output rows arrive as 40, 14 or 5 runs (one
-    ncclSend to itself and one ncclRecv into the frame rows per run, the last 3-row run partial), bit for bit
-    the plain context's image."""
+    """The 1-device RCCL group at several block sizes (40 output rows as 40, 14 or 5 runs of 1, 3 or 8 rows, the
+    last 3-row run partial): the part's tile goes to rank 0 in one ncclSend to itself, is received into the
+    staging buffer and placed into its frame rows, bit for bit the plain context's image."""
     scene = _scene(R, "c3_s1024_reflect.yaml", 48, 40, 1)
     single.upload(scene)
     ref = single.render(scene.camera, aa=1)
