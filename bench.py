@@ -642,8 +642,9 @@ def dry_run(args, world, mode, workload):
         avg = o.aa_average(np.nan_to_num(canvas), aa)
         out[: len(rows)] = torch.from_numpy(avg[rows])
 
-    # multi.cpp's layout: f64 tiles padded to part 0's row count, gathered back to back on rank 0 and
-    # un-interleaved by the library's rr_unshuffle_host (the device kernel's index arithmetic)
+    # multi.cpp's layout: unpadded f64 tiles, one send per part to rank 0, received back to back into a staging
+    # buffer (part p at rr_stage_row_offset) and placed by the library's rr_unshuffle_host (the runs the device
+    # placement kernels move)
     pipe = rdist.FramePipeline(H, W, 3, torch.float64, torch.device("cpu"), block=BLOCK) if (tiles and distributed) \
         else None
     t0 = time.perf_counter()
@@ -667,7 +668,7 @@ def dry_run(args, world, mode, workload):
         elapsed = float(t.item())
     identity = None
     if pipe is not None:  # one more frame through the library's host un-interleave (rr_unshuffle_host)
-        tile = torch.zeros((rdist.max_tile_rows(H, world, BLOCK), W, 3), dtype=torch.float64)
+        tile = torch.zeros((len(rows), W, 3), dtype=torch.float64)
         render_tile(tile)
         via_lib = rdist.gather_frame(tile, H, BLOCK)
     if rank == 0 and pipe is not None:
@@ -675,7 +676,8 @@ def dry_run(args, world, mode, workload):
         ref = o.aa_average(np.nan_to_num(full), aa)
         identity = {"bit_identical_to_1_part": bool(np.array_equal(pipe.frame.numpy(), ref)),
                     "rr_unshuffle_host_bit_identical": bool(np.array_equal(via_lib.numpy(), ref)),
-                    "layout": "multi.cpp: padded f64 tiles back to back (ncclGather layout), library un-interleave"}
+                    "layout": "multi.cpp: unpadded f64 tiles, one send / receive per part into the staging "
+                              "buffer at rr_stage_row_offset, library run placement (rr_unshuffle_host)"}
     if rank == 0:
         frames_per_step = world if not tiles else 1
         line = {"metric": METRIC, "value": round(frames_per_step * W * H * aa * aa * steps / elapsed / 1e6, 6),

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 8
+#define RR_ABI_VERSION 9
 
 /* error codes */
 #define RR_OK 0
@@ -176,8 +176,10 @@ int rr_scene_upload(rr_ctx* ctx, const rr_scene_desc* desc);
 
 /* ---- multi-device contexts (ABI 5): one frame across several GPUs (camera.rs:107-121 spreads one
  * frame over every rayon worker).  Global rank r renders the output rows {y : (y/block_rows) % N == r}
- * as an f64 AA-averaged tile; one RCCL group of point-to-point operations (over xGMI) brings every
- * 8-row run of every tile straight into its frame rows on rank 0 (no permutation pass).  The context
+ * as an f64 AA-averaged tile.  One RCCL group per frame (over xGMI): every rank sends its whole tile to
+ * rank 0 in one ncclSend, and rank 0 receives every part's tile (its own from itself) back to back into a
+ * staging buffer of `height` rows, one ncclRecv per part (part p at row rr_stage_row_offset); one copy
+ * kernel per part then places the tile's rows into their frame rows on the transfer stream.  The context
  * owns a render and a transfer stream per device and the RCCL communicator.  rr_render (blocking; out_avg filled on rank 0 only) and
  * rr_render_gather_device (asynchronous) take part 0 of 1: the context does the split.  Only the
  * f64 averaged image is produced (no RR_OUT_CANVAS / RR_OUT_AVG_F32).  rr_color_at / rr_is_shadowed /
@@ -192,21 +194,25 @@ int rr_create_rank(int device, int nranks, int rank, const uint8_t* unique_id, r
 /* nranks in the group, this context's first global rank, devices this context drives (1/0/1 for rr_create) */
 int rr_context_info(const rr_ctx* ctx, int32_t* nranks, int32_t* rank, int32_t* ndevices);
 /* ABI 7: nparts VIRTUAL ranks on one device — the N > 1 path of a real group (per-part contexts and
- * streams, tiles, double buffering) with the RCCL transfer replaced by a device-local copy of every run
- * into its frame rows.  For exercising / testing the multi-GPU
- * frame assembly on one GPU; images are bit-identical to one part's. */
+ * streams, tiles, double buffering, the staging buffer at the same per-part offsets and the same placement
+ * kernels) with only the ncclSend / ncclRecv pairs replaced by device-local copies of each tile into the
+ * staging buffer.  For exercising / testing the multi-GPU frame assembly on one GPU; images are
+ * bit-identical to one part's. */
 int rr_create_virtual(int device, int nparts, rr_ctx** out);
-/* ABI 7: the frame from tiles a caller gathered itself (e.g. torch.distributed.gather; the same run
- * arithmetic as the device transfer): gathered = nparts tiles back to back, each rr_part_rows(height, 0, nparts, block_rows, NULL) rows of
- * width*3 doubles (part p's rows in increasing y, padded) -> frame = height rows in frame order.  No
- * device needed (CPU rehearsals of the N > 1 path use it).  The buffers are not checked: `gathered` must
- * hold nparts * tile_rows * width * 3 doubles and `frame` height * width * 3 (rray_amd.unshuffle checks
- * its array's shape before the call). */
+/* ABI 9: first row of part `part`'s tile in the staging buffer (the rows of parts 0 .. part-1; partition.hpp
+ * stage_row_offset).  part == nparts gives height. */
+int64_t rr_stage_row_offset(int64_t height, int32_t part, int32_t nparts, int32_t block_rows);
+/* ABI 9 (was ABI 7 with padded tiles): the frame from tiles a caller transferred itself (e.g. torch.distributed
+ * send / recv; the same layout and run arithmetic as the device transfer): staged = the nparts tiles back to back,
+ * unpadded, part p's rows (increasing y) at row rr_stage_row_offset(height, p, nparts, block_rows), height rows of
+ * width*3 doubles in all -> frame = height rows in frame order.  No device needed (CPU rehearsals of the N > 1 path
+ * use it).  The buffers are not checked: both must hold height * width * 3 doubles (rray_amd.unshuffle checks its
+ * array's shape before the call). */
+int rr_unshuffle_host(const double* staged, double* frame, int64_t width, int64_t height, int32_t nparts,
+                      int32_t block_rows);
 /* ABI 8: build provenance — the sha256 prefix of the product sources this library was built from
  * (rray_amd/build.py source_digest(): rray_amd/csrc/*, this header, the build script).  Static string. */
 const char* rr_build_digest(void);
-int rr_unshuffle_host(const double* gathered, double* frame, int64_t width, int64_t height, int32_t nparts,
-                      int32_t block_rows);
 /* Whole frame -> d_frame (W*H*3 doubles on rank 0's device; ignored on other ranks), enqueued after
  * the work already on `hip_stream` (NULL: no ordering with the caller) and completed in its order;
  * not synchronised.  Collective: every rank calls it for every frame.  Tiles are double-buffered, so
@@ -233,9 +239,10 @@ int rr_render_device(rr_ctx* ctx, const rr_camera* cam, const rr_render_opts* op
 int64_t rr_part_rows(int64_t height, int32_t part, int32_t nparts, int32_t block_rows, int64_t* rows_out);
 /* Per-kernel HIP-event timing on the context's stream.  rr_kernel_profile(ctx, 1) resets and enables
  * it; rr_kernel_times fills accumulated milliseconds and launch counts per kernel in the order
- * trace, n1n2, shade, shadow, finish, combine, aa, trace_shade (returns the number of kernels, 8;
- * the shadow walks and the light sum run inside shade, so shadow and finish stay 0; scenes without
- * transparent materials run trace and shade as one trace_shade kernel). */
+ * trace, n1n2, shade, shadow, finish, combine, aa, trace_shade, chain, deep (returns the number of kernels,
+ * 10; the shadow walks and the light sum run inside shade, so shadow and finish stay 0; scenes without
+ * transparent materials run trace and shade as one trace_shade kernel, and those whose materials reflect run
+ * every reflection chain in one chain kernel — deep only with RRAY_DEEP=1). */
 int rr_kernel_profile(rr_ctx* ctx, int enable);
 int rr_kernel_times(rr_ctx* ctx, double* ms, uint64_t* launches, int32_t n);
 /* stats of the last rr_render/rr_render_device on this context (synchronises) */

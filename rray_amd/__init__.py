@@ -17,10 +17,11 @@ from .render import (  # noqa: F401
     rccl_unique_id,
     render_scene_from_file,
     render_scene_from_str,
+    stage_row_offset,
     unshuffle,
     write_png,
 )
 
 __all__ = ["Renderer", "SceneBuilder", "YamlScene", "camera", "part_rows", "quantize", "write_png",
-           "render_scene_from_str", "render_scene_from_file", "device_count", "rccl_unique_id", "unshuffle", "RRError",
+           "render_scene_from_str", "render_scene_from_file", "device_count", "rccl_unique_id", "stage_row_offset", "unshuffle", "RRError",
            "lib"]

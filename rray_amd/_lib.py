@@ -76,7 +76,7 @@ EXPORTS = ["rr_abi_version", "rr_last_error", "rr_device_count", "rr_create", "r
            "rr_is_shadowed", "rr_scene_inspect", "rr_scene_from_yaml", "rr_scene_desc_of", "rr_scene_free", "rr_quantize",
            "rr_write_png", "rr_render_scene_from_file", "rr_render_scene_from_file_devices", "rr_create_multi",
            "rr_rccl_unique_id", "rr_create_rank", "rr_context_info", "rr_render_gather_device", "rr_create_virtual",
-           "rr_unshuffle_host", "rr_build_digest"]
+           "rr_unshuffle_host", "rr_stage_row_offset", "rr_build_digest"]
 RCCL_ID_BYTES = 128
 
 _lib = None
@@ -130,6 +130,8 @@ def lib():
     L.rr_context_info.argtypes = [C.c_void_p, _I, _I, _I]
     L.rr_create_virtual.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
     L.rr_unshuffle_host.argtypes = [_D, _D, C.c_int64, C.c_int64, C.c_int32, C.c_int32]
+    L.rr_stage_row_offset.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_int32]
+    L.rr_stage_row_offset.restype = C.c_int64
     L.rr_render_gather_device.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(RenderOpts), C.c_void_p,
                                           C.c_void_p]
     L.rr_build_digest.restype = C.c_char_p

@@ -899,15 +899,23 @@ int64_t rr_part_rows(int64_t height, int32_t part, int32_t nparts, int32_t block
     return n;
 }
 
-int rr_unshuffle_host(const double* gathered, double* frame, int64_t width, int64_t height, int32_t nparts,
+int64_t rr_stage_row_offset(int64_t height, int32_t part, int32_t nparts, int32_t block) {
+    if (height < 0 || nparts < 1 || block < 1 || part < 0 || part > nparts)
+        return fail(RR_E_ARG, "rr_stage_row_offset: bad arguments");
+    return rr::stage_row_offset(height, part, nparts, block);
+}
+
+int rr_unshuffle_host(const double* staged, double* frame, int64_t width, int64_t height, int32_t nparts,
                       int32_t block) {
-    if (!gathered || !frame || width < 0 || height < 0 || nparts < 1 || block < 1)
+    if (!staged || !frame || width < 0 || height < 0 || nparts < 1 || block < 1)
         return fail(RR_E_ARG, "rr_unshuffle_host: bad arguments");
-    const int64_t tile_rows = rr::gather_tile_rows(height, nparts, block), row = width * 3;
-    for (int32_t p = 0; p < nparts; ++p)  // the runs rank 0's receives place (partition.hpp)
+    const int64_t row = width * 3;
+    for (int32_t p = 0; p < nparts; ++p) {  // the runs place_tile_kernel moves on rank 0 (partition.hpp)
+        const double* tile = staged + rr::stage_row_offset(height, p, nparts, block) * row;
         rr::for_each_part_run(height, p, nparts, block, [&](int64_t j, int64_t y, int64_t n) {
-            std::memcpy(frame + y * row, gathered + (p * tile_rows + j) * row, (size_t)(n * row) * sizeof(double));
+            std::memcpy(frame + y * row, tile + j * row, (size_t)(n * row) * sizeof(double));
         });
+    }
     return RR_OK;
 }
 

@@ -1,30 +1,32 @@
-// multi.cpp — multi-device render contexts: row-interleaved tiles received straight into frame order
-// (DESIGN.md §5).
+// multi.cpp — multi-device render contexts: row-interleaved tiles, one RCCL transfer per part into a staging
+// buffer, placed into frame order on rank 0.
 //
 // Camera::render (camera.rs:107-121) spreads one frame over every rayon worker; here one frame is
 // spread over GPUs.  Global rank r renders the output rows {y : (y / block) % nranks == r} (the
-// interleaving balances sky and floor cost) as an f64 AA-averaged tile in its own HBM.  The tile is a
-// sequence of runs (one 8-row block each) that are contiguous in the frame, so the transfer needs no
-// permutation pass: inside one RCCL group every rank sends its runs to rank 0 (ncclSend, over xGMI) and
-// rank 0 posts one ncclRecv per run of every part straight into that run's frame rows — its own part
-// included, as a send to itself.  Two tile buffers alternate so that rendering frame k+1 overlaps the
-// transfer of frame k: a render waits only for the transfer that last read its buffer.  Each part also
-// alternates between two render contexts (scene copy + level workspace) on two render streams, so frame
-// k+1's camera level runs beside frame k's deep levels, whose few incoherent waves leave the GPU mostly idle
-// (with a row tile of C3 per GPU the deep levels are a latency floor per frame, tools/part_scaling.py).
+// interleaving balances sky and floor cost) as an f64 AA-averaged tile in its own HBM.  Inside one RCCL group
+// per frame every rank sends its whole tile to rank 0 in one ncclSend (over xGMI), and rank 0 receives every
+// part's tile — its own included, as a send to itself — back to back into a staging buffer of `height` rows
+// (part p at partition.hpp stage_row_offset(p)), one ncclRecv per part; one copy kernel per part then places the
+// tile's runs into their frame rows (frame_row_of).  Two tile buffers alternate so that rendering frame k+1
+// overlaps the transfer of frame k: a render waits only for the transfer that last read its buffer.  Each part
+// also alternates between two render contexts (scene copy + level workspace) on two render streams.
 //
-// Two shapes of the same group: rr_create_multi (this process drives n devices, ncclCommInitAll,
-// ncclGroupStart/End around every device's operations) and rr_create_rank (one process per GPU,
-// ncclCommInitRank from an id made by rr_rccl_unique_id on rank 0 and shared by the host).  A virtual group
-// (rr_create_virtual: every part on one device) places each tile's runs with a copy kernel instead.
+// Three shapes of the same group: rr_create_multi (this process drives n devices, ncclCommInitAll,
+// ncclGroupStart/End around every device's operations), rr_create_rank (one process per GPU, ncclCommInitRank
+// from an id made by rr_rccl_unique_id on rank 0 and shared by the host) and rr_create_virtual (every part on one
+// device, no communicator): a virtual group runs the same staging buffer, offsets and placement kernels, with a
+// device-local copy of each tile into its stage rows standing in for the send / receive pair.
 #include "multi.hpp"
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "device_guard.hpp"
@@ -69,8 +71,8 @@ struct DevMem {
     }
 };
 
-// A tile's rows -> their frame rows (partition.hpp frame_row_of): the virtual group's transfer.  One thread
-// per double; both sides are contiguous along a row.
+// A tile's rows in the staging buffer -> their frame rows (partition.hpp frame_row_of), on the root after the
+// transfer.  One thread per double; both sides are contiguous along a row.
 __global__ void __launch_bounds__(256) place_tile_kernel(const double* __restrict__ tile, double* __restrict__ out,
                                                          int64_t row_len, int64_t rows, int32_t part, int32_t nparts,
                                                          int32_t block) {
@@ -98,11 +100,11 @@ struct rr_group {
     std::vector<ncclComm_t> comms;
     std::vector<hipStream_t> render_st[2], comm_st;
     std::vector<hipEvent_t> ev_rendered[2], ev_gathered[2];
-    bool virt = false;                    // rr_create_virtual: every part on one device, transfer = local copies
+    bool virt = false;                    // rr_create_virtual: every part on one device, send/recv = local copies
     hipEvent_t ev_caller = nullptr;       // root: the caller's stream position at the gather call
     std::vector<DevMem> tile[2];          // per local part: its tile (rows of the part, in tile order)
     DevMem frame;                         // root: assembled frame for the blocking rr_render
-    DevMem stage;                         // root of an RCCL group: every part's tile, received back to back
+    DevMem stage;                         // root: every part's tile back to back (part p at stage_row_offset(p))
     int64_t k = 0;                        // frames issued (buffer and render context = k % 2)
     int nlocal() const { return (int)devices.size(); }
     int last() const { return k > 0 ? (int)((k - 1) & 1) : 0; }  // the set that rendered the latest frame
@@ -229,15 +231,40 @@ int group_create_virtual(int device, int nparts, rr_group** out) {
     return RR_OK;
 }
 
-void group_destroy(rr_group* g) {
-    DeviceGuard device_guard;
-    if (!g) return;
+// Waits for a stream to drain.  A stream that is still busy after 30 s is named on stderr (once) before the wait
+// goes on: work still enqueued at teardown means an earlier call returned without draining it, or a kernel
+// that does not end — either way the name says which part and stream, where a bare hang would not (DESIGN.md §5,
+// the round-4 teardown hang).
+static void drain_stream(hipStream_t st, const char* what, size_t part, int set) {
+    if (!st) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    bool told = false;
+    for (;;) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e != hipErrorNotReady) return;  // done, or failed (then nothing more completes on it)
+        if (!told && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+            std::fprintf(stderr, "rray: group teardown: %s stream of part %zu (set %d) still busy after 30 s\n", what,
+                         part, set);
+            told = true;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+
+// Every stream of the group drained: the render streams of both sets and the transfer streams.
+static void group_drain(rr_group* g) {
     for (size_t l = 0; l < g->devices.size(); ++l) {
         (void)hipSetDevice(g->devices[l]);
         for (int b = 0; b < 2; ++b)
-            if (l < g->render_st[b].size() && g->render_st[b][l]) (void)hipStreamSynchronize(g->render_st[b][l]);
-        if (l < g->comm_st.size() && g->comm_st[l]) (void)hipStreamSynchronize(g->comm_st[l]);
+            if (l < g->render_st[b].size()) drain_stream(g->render_st[b][l], "render", l, b);
+        if (l < g->comm_st.size()) drain_stream(g->comm_st[l], "transfer", l, -1);
     }
+}
+
+void group_destroy(rr_group* g) {
+    DeviceGuard device_guard;
+    if (!g) return;
+    group_drain(g);
     for (ncclComm_t c : g->comms)
         if (c) (void)ncclCommDestroy(c);
     for (size_t l = 0; l < g->devices.size(); ++l) {
@@ -276,6 +303,81 @@ int group_upload(rr_group* g, const rr_scene_desc* d) {
     return RR_OK;
 }
 
+// Enqueues one frame: every local part's render into its tile buffer of set b, the transfer into the staging
+// buffer (RCCL send / receive pairs, or a virtual group's device copies) and, on the root, the placement kernels
+// into `frame`.  `enqueued` turns true with the first enqueued operation: the caller drains the group when this
+// returns an error after that point, so no work outlives a failed call.
+static int enqueue_frame(rr_group* g, const rr_camera* cam, const std::vector<rr_render_opts>& opts, double* frame,
+                         hipStream_t caller, int64_t W, int64_t H, int32_t block, int b, bool& enqueued) {
+    const int n = g->nlocal();
+    const int64_t row = W * 3;
+    for (int l = 0; l < n; ++l) {
+        GHIP(hipSetDevice(g->devices[l]));
+        // the transfer that last read this buffer (two frames ago) must be done before it is overwritten; the
+        // render context and stream of set b are free once that frame's render is (same stream)
+        GHIP(hipStreamWaitEvent(g->render_st[b][l], g->ev_gathered[b][l], 0));
+        enqueued = true;
+        int rc = rr_render_device(g->subs[b][l], cam, &opts[l], nullptr, g->tile[b][l].p, g->render_st[b][l]);
+        if (rc != RR_OK) return rc;
+        GHIP(hipEventRecord(g->ev_rendered[b][l], g->render_st[b][l]));
+        GHIP(hipStreamWaitEvent(g->gather_stream(l), g->ev_rendered[b][l], 0));
+    }
+    double* stage = g->root_here() ? static_cast<double*>(g->stage.p) : nullptr;
+    if (g->virt) {
+        // the send / receive pairs of a real group, as device-local copies: part l's tile into its stage rows, on
+        // the root's transfer stream (where the receives run)
+        GHIP(hipSetDevice(g->devices[0]));
+        for (int l = 0; l < n; ++l) {
+            const int64_t rows = part_rows_count(H, l, g->nranks, block);
+            if (rows > 0)
+                GHIP(hipMemcpyAsync(stage + stage_row_offset(H, l, g->nranks, block) * row, g->tile[b][l].p,
+                                    (size_t)(rows * row) * sizeof(double), hipMemcpyDeviceToDevice, g->comm_st[0]));
+        }
+    } else {
+        // one RCCL group per frame: each local part sends its whole tile to rank 0 in one ncclSend, and rank 0
+        // receives every part's tile (its own from itself) into its stage rows.  One operation per part: the round-4
+        // first cut posted one send / receive per 8-row run (270 per C3 frame on rank 0), and the per-operation cost
+        // made the one-rank group's frame 1.49 ms slower than the single render (7.83 vs 6.34 ms).  The group is
+        // always closed, also when posting an operation fails.
+        ncclResult_t r = ncclGroupStart();
+        if (r == ncclSuccess) {
+            for (int l = 0; l < n && r == ncclSuccess; ++l) {
+                const int64_t rows = part_rows_count(H, g->rank0 + l, g->nranks, block);
+                if (rows > 0)
+                    r = ncclSend(g->tile[b][l].p, (size_t)(rows * row), ncclFloat64, 0, g->comms[l], g->comm_st[l]);
+                if (!(g->root_here() && l == 0)) continue;
+                for (int32_t p = 0; p < g->nranks && r == ncclSuccess; ++p) {
+                    const int64_t pr = part_rows_count(H, p, g->nranks, block);
+                    if (pr > 0)
+                        r = ncclRecv(stage + stage_row_offset(H, p, g->nranks, block) * row, (size_t)(pr * row),
+                                     ncclFloat64, p, g->comms[0], g->comm_st[0]);
+                }
+            }
+            const ncclResult_t e = ncclGroupEnd();
+            if (r == ncclSuccess) r = e;
+        }
+        if (r != ncclSuccess) return gfail(RR_E_HIP, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
+    }
+    if (g->root_here()) {
+        GHIP(hipSetDevice(g->devices[0]));
+        // d_frame is written in the caller's stream order: only the placement waits for it (the receives into the
+        // private stage do not, so peers' sends never wait on unrelated caller work)
+        if (caller) GHIP(hipStreamWaitEvent(g->comm_st[0], g->ev_caller, 0));
+        for (int32_t p = 0; p < g->nranks; ++p)
+            GHIP(launch_place_tile(stage + stage_row_offset(H, p, g->nranks, block) * row, frame, W,
+                                   part_rows_count(H, p, g->nranks, block), p, g->nranks, block, g->comm_st[0]));
+    }
+    for (int l = 0; l < n; ++l) {  // a virtual group's tiles are all read on comm_st[0]
+        GHIP(hipSetDevice(g->devices[l]));
+        GHIP(hipEventRecord(g->ev_gathered[b][l], g->gather_stream(l)));
+    }
+    if (g->root_here() && caller) {
+        GHIP(hipSetDevice(g->devices[0]));
+        GHIP(hipStreamWaitEvent(caller, g->ev_gathered[b][0], 0));
+    }
+    return RR_OK;
+}
+
 int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts* o, void* d_frame, void* stream) {
     DeviceGuard device_guard;
     if (!cam || !o) return gfail(RR_E_ARG, "null camera/options");
@@ -304,78 +406,24 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
         GHIP(hipSetDevice(g->devices[l]));
         GHIP(g->tile[b][l].ensure((size_t)part_rows_count(H, so.part, g->nranks, block) * (size_t)row * sizeof(double)));
     }
-    if (g->root_here() && !g->virt) {  // the receive staging buffer (the whole frame's rows), before any work is enqueued
+    if (g->root_here()) {  // the staging buffer (the whole frame's rows), before any work is enqueued
         GHIP(hipSetDevice(g->devices[0]));
         GHIP(g->stage.ensure((size_t)H * (size_t)row * sizeof(double)));
     }
-    if (g->root_here() && stream) {
+    hipStream_t caller = g->root_here() ? (hipStream_t)stream : nullptr;
+    if (caller) {
         GHIP(hipSetDevice(g->devices[0]));
-        GHIP(hipEventRecord(g->ev_caller, (hipStream_t)stream));
+        GHIP(hipEventRecord(g->ev_caller, caller));
     }
-    for (int l = 0; l < n; ++l) {
-        GHIP(hipSetDevice(g->devices[l]));
-        // the transfer that last read this buffer (two frames ago) must be done before it is overwritten; the
-        // render context and stream of set b are free once that frame's render is (same stream)
-        GHIP(hipStreamWaitEvent(g->render_st[b][l], g->ev_gathered[b][l], 0));
-        int rc = rr_render_device(g->subs[b][l], cam, &opts[l], nullptr, g->tile[b][l].p, g->render_st[b][l]);
-        if (rc != RR_OK) return rc;
-        GHIP(hipEventRecord(g->ev_rendered[b][l], g->render_st[b][l]));
-        GHIP(hipStreamWaitEvent(g->gather_stream(l), g->ev_rendered[b][l], 0));
-    }
-    double* frame = static_cast<double*>(d_frame);
-    if (g->root_here() && stream) {  // d_frame is written in the caller's stream order
-        GHIP(hipSetDevice(g->devices[0]));
-        GHIP(hipStreamWaitEvent(g->comm_st[0], g->ev_caller, 0));
-    }
-    if (g->virt) {
-        GHIP(hipSetDevice(g->devices[0]));
-        for (int l = 0; l < n; ++l)
-            GHIP(launch_place_tile(static_cast<const double*>(g->tile[b][l].p), frame, W,
-                                   part_rows_count(H, l, g->nranks, block), l, g->nranks, block, g->comm_st[0]));
-    } else {
-        // one RCCL group per frame: each local part sends its whole tile to rank 0 in one ncclSend, and rank 0
-        // receives every part's tile (its own from itself) back to back into the staging buffer, then places each
-        // tile's rows into their frame rows with one copy kernel per part on the same stream (HBM-bound, ~2 x 199
-        // MB per C3 frame, overlapped with the next frame's render).  One operation per part: the round-4 first
-        // cut posted one send / receive per 8-row run (270 per C3 frame on rank 0), and the per-operation cost
-        // made the one-rank group's frame 1.49 ms slower than the single render (7.83 vs 6.34 ms).  The group is
-        // always closed, also when posting an operation fails.
-        double* stage = g->root_here() ? static_cast<double*>(g->stage.p) : nullptr;
-        ncclResult_t r = ncclGroupStart();
-        if (r == ncclSuccess) {
-            for (int l = 0; l < n && r == ncclSuccess; ++l) {
-                const int64_t rows = part_rows_count(H, g->rank0 + l, g->nranks, block);
-                if (rows > 0)
-                    r = ncclSend(g->tile[b][l].p, (size_t)(rows * row), ncclFloat64, 0, g->comms[l], g->comm_st[l]);
-                if (!(g->root_here() && l == 0)) continue;
-                int64_t off = 0;
-                for (int32_t p = 0; p < g->nranks && r == ncclSuccess; ++p) {
-                    const int64_t pr = part_rows_count(H, p, g->nranks, block);
-                    if (pr > 0) r = ncclRecv(stage + off * row, (size_t)(pr * row), ncclFloat64, p, g->comms[0], g->comm_st[0]);
-                    off += pr;
-                }
-            }
-            const ncclResult_t e = ncclGroupEnd();
-            if (r == ncclSuccess) r = e;
+    bool enqueued = false;
+    const int rc = enqueue_frame(g, cam, opts, static_cast<double*>(d_frame), caller, W, H, block, b, enqueued);
+    if (rc != RR_OK) {
+        if (enqueued) {  // drain what this call enqueued before reporting: nothing of a failed frame stays in flight
+            const std::string msg = rr_last_error();
+            group_drain(g);
+            rr_set_error(msg.c_str());
         }
-        if (r != ncclSuccess) return gfail(RR_E_HIP, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
-        if (g->root_here()) {
-            GHIP(hipSetDevice(g->devices[0]));
-            int64_t off = 0;
-            for (int32_t p = 0; p < g->nranks; ++p) {
-                const int64_t pr = part_rows_count(H, p, g->nranks, block);
-                GHIP(launch_place_tile(stage + off * row, frame, W, pr, p, g->nranks, block, g->comm_st[0]));
-                off += pr;
-            }
-        }
-    }
-    for (int l = 0; l < n; ++l) {  // a virtual group's tiles are all read on comm_st[0]
-        GHIP(hipSetDevice(g->devices[l]));
-        GHIP(hipEventRecord(g->ev_gathered[b][l], g->gather_stream(l)));
-    }
-    if (g->root_here() && stream) {
-        GHIP(hipSetDevice(g->devices[0]));
-        GHIP(hipStreamWaitEvent((hipStream_t)stream, g->ev_gathered[b][0], 0));
+        return rc;
     }
     ++g->k;
     return RR_OK;
@@ -398,10 +446,20 @@ int group_render(rr_group* g, const rr_camera* cam, const rr_render_opts* o, dou
     so.flags = RR_OUT_AVG;
     int rc = group_render_gather(g, cam, &so, g->root_here() ? g->frame.p : nullptr, nullptr);
     if (rc != RR_OK) return rc;
-    for (int l = 0; l < g->nlocal(); ++l) {
+    for (int l = 0; l < g->nlocal(); ++l) {  // every stream synchronised: a failure here leaves nothing in flight either
         GHIP(hipSetDevice(g->devices[l]));
-        for (int b = 0; b < 2; ++b) GHIP(hipStreamSynchronize(g->render_st[b][l]));
-        GHIP(hipStreamSynchronize(g->comm_st[l]));
+        for (int b = 0; b < 2; ++b) {
+            const hipError_t e = hipStreamSynchronize(g->render_st[b][l]);
+            if (e != hipSuccess) {
+                group_drain(g);
+                return gfail(RR_E_HIP, std::string("hipStreamSynchronize(render): ") + hipGetErrorString(e));
+            }
+        }
+        const hipError_t e = hipStreamSynchronize(g->comm_st[l]);
+        if (e != hipSuccess) {
+            group_drain(g);
+            return gfail(RR_E_HIP, std::string("hipStreamSynchronize(transfer): ") + hipGetErrorString(e));
+        }
     }
     if (g->root_here() && out_avg && (o->flags & RR_OUT_AVG)) {
         GHIP(hipSetDevice(g->devices[0]));

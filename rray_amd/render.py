@@ -226,17 +226,24 @@ def part_rows(height, part, nparts, block_rows=8):
     return out[:n]
 
 
-def unshuffle(gathered, height, nparts, block_rows=8):
-    """rr_unshuffle_host: the root's un-interleave on the host.  gathered: (nparts * tile_rows, W, 3) f64 in
-    ncclGather's layout (tile_rows = len(part_rows(height, 0, nparts, block_rows)))."""
-    g = np.ascontiguousarray(gathered, np.float64)
+def stage_row_offset(height, part, nparts, block_rows=8):
+    """rr_stage_row_offset: first row of part `part`'s tile in the staging buffer (the rows of parts below it)."""
+    n = lib().rr_stage_row_offset(height, part, nparts, block_rows)
+    if n < 0:
+        check(int(n))
+    return int(n)
+
+
+def unshuffle(staged, height, nparts, block_rows=8):
+    """rr_unshuffle_host: the root's un-interleave on the host.  staged: (height, W, 3) f64, the parts' tiles back to
+    back and unpadded, part p's rows at stage_row_offset(height, p, nparts, block_rows) — the staging buffer the
+    library's per-part receives fill on rank 0 (multi.cpp)."""
+    g = np.ascontiguousarray(staged, np.float64)
     if nparts < 1 or block_rows < 1 or height < 0:
         raise ValueError(f"unshuffle: bad partition (height {height}, nparts {nparts}, block_rows {block_rows})")
-    tile_rows = len(part_rows(height, 0, nparts, block_rows))
-    # the library reads nparts * tile_rows rows of W * 3 doubles: refuse any other buffer before it does
-    if g.ndim != 3 or g.shape[0] != nparts * tile_rows or g.shape[2] != 3:
-        raise ValueError(f"unshuffle: gathered must have shape ({nparts * tile_rows}, W, 3) for height {height}, "
-                         f"{nparts} parts of block_rows {block_rows}; got {g.shape}")
+    # the library reads height rows of W * 3 doubles: refuse any other buffer before it does
+    if g.ndim != 3 or g.shape[0] != height or g.shape[2] != 3:
+        raise ValueError(f"unshuffle: staged must have shape ({height}, W, 3) for height {height}; got {g.shape}")
     W = g.shape[1]
     frame = np.zeros((height, W, 3), np.float64)
     check(lib().rr_unshuffle_host(_dp(g), _dp(frame), W, height, nparts, block_rows))

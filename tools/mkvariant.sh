@@ -11,7 +11,7 @@ cp -r rray_amd/csrc "$tmp/a/rray_amd/"; cp -r rray_amd/csrc "$tmp/b/rray_amd/"
 while [ $# -ge 2 ]; do
   sed -i "$2" "$tmp/b/rray_amd/csrc/$1"; shift 2
 done
-(cd "$tmp" && diff -ru a b > "$OLDPWD/tools/patches/$name.patch") || true
+(cd "$tmp" && diff -ru -x '*.orig' a b > "$OLDPWD/tools/patches/$name.patch") || true
 rm -rf "$tmp"
 test -s "tools/patches/$name.patch" || { echo "empty patch"; exit 1; }
 python -c "import sys; sys.path.insert(0, '.'); from rray_amd import build; print(build.build_variant('$name', [], patch='tools/patches/$name.patch'))"
