@@ -48,11 +48,41 @@ def source_digest():
     return h.hexdigest()[:16]
 
 
-def _deps_mtime():
+def _dep_files():
+    """Every file a unit may include: the csrc headers and .inc files and the public header (a unit's key hashes
+    them all — a conservative include set, so no header edit can leave a stale object behind)."""
     files = glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(os.path.join(CSRC, "*.inc"))
     files += glob.glob(os.path.join(ROOT, "include", "rray", "*.h"))
-    files.append(os.path.abspath(__file__))
-    return max(os.path.getmtime(f) for f in files)
+    return sorted(files)
+
+
+def _sha(paths, extra=""):
+    import hashlib
+
+    h = hashlib.sha256(extra.encode())
+    for f in paths:
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def unit_key(path, deps, cmd):
+    """Content key of one object: the unit's source, every file it may include and the compile command.  An object
+    is rebuilt whenever its recorded key differs — modification times play no part, so a tree restored with old
+    mtimes (tar, rsync -t) next to newer stale objects still recompiles, and a digest match proves the objects came
+    from these sources."""
+    return _sha([path] + list(deps), "\0".join(cmd))
+
+
+def _key_file(out):
+    return out + ".key"
+
+
+def _key_matches(out, key):
+    kf = _key_file(out)
+    return os.path.exists(out) and os.path.exists(kf) and open(kf).read().strip() == key
 
 
 REMARKS = ["-Rpass-analysis=kernel-resource-usage"]  # per-kernel VGPR / spill report (codegen unchanged)
@@ -106,16 +136,19 @@ def check_cross_lane(resource_files):
     return names
 
 
-def _compile(src, deps_mtime, verbose):
+def _compile(src, deps, verbose):
     out = os.path.join(OBJ, os.path.splitext(src)[0] + ".o")
     path = os.path.join(CSRC, src)
-    if os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(path), deps_mtime):
-        return out
     cmd = [HIPCC] + COMMON + DEVICE + UNIT_FLAGS.get(src, []) + ["-c", path, "-o", out]
     if src.endswith(".cpp"):
         cmd = [HIPCC, "-x", "hip"] + COMMON + DEVICE + ["-c", path, "-o", out]
     else:
         cmd += REMARKS
+    key = unit_key(path, deps, cmd)
+    if _key_matches(out, key) and (src.endswith(".cpp") or os.path.exists(out + ".resources.json")):
+        return out
+    if os.path.exists(_key_file(out)):
+        os.remove(_key_file(out))  # a failed compile leaves no key behind
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -123,6 +156,8 @@ def _compile(src, deps_mtime, verbose):
         raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
     if src.endswith(".hip"):
         json.dump(_resources(r.stderr), open(out + ".resources.json", "w"))
+    with open(_key_file(out), "w") as fh:
+        fh.write(key + "\n")
     return out
 
 
@@ -183,13 +218,16 @@ def _digest_object(verbose=False, out_dir=None, digest=None):
             f'extern "C" const char* rr_build_digest(void) {{ return "{d}"; }}\n')
     if not os.path.exists(src) or open(src).read() != text:
         open(src, "w").write(text)
-    if not os.path.exists(obj) or os.path.getmtime(obj) < os.path.getmtime(src):
-        cmd = ["g++", "-O2", "-fPIC", "-c", src, "-o", obj]
+    cmd = ["g++", "-O2", "-fPIC", "-c", src, "-o", obj]
+    key = unit_key(src, [], cmd)
+    if not _key_matches(obj, key):
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"compile failed: build_digest.cpp\n{r.stderr}")
+        with open(_key_file(obj), "w") as fh:
+            fh.write(key + "\n")
     return obj
 
 
@@ -197,25 +235,31 @@ def build(verbose=False, jobs=None):
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
     os.makedirs(BINDIR, exist_ok=True)
-    dm = _deps_mtime()
+    deps = _dep_files()
     jobs = jobs or min(len(SOURCES), max(1, min(16, os.cpu_count() or 1)))
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, dm, verbose), SOURCES))
+        objs = list(ex.map(lambda s: _compile(s, deps, verbose), SOURCES))
     check_cross_lane([o + ".resources.json" for o in objs if o.endswith(".o") and os.path.exists(o + ".resources.json")])
     objs.append(_digest_object(verbose))
-    newest = max(os.path.getmtime(o) for o in objs)
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
-        cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", LIB] + objs + ["-lz", "-L/opt/rocm/lib", "-lrccl", "-Wl,-soname,librray_amd.so"]
+    # the library's key: the link command over the objects' own keys (each the content of its sources)
+    cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", LIB] + objs + ["-lz", "-L/opt/rocm/lib", "-lrccl", "-Wl,-soname,librray_amd.so"]
+    lib_key = _sha([_key_file(o) for o in objs], "\0".join(cmd))
+    if not _key_matches(LIB, lib_key):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
+        with open(_key_file(LIB), "w") as fh:
+            fh.write(lib_key + "\n")
     cli_src = os.path.join(CSRC, "cli.cpp")
-    if not os.path.exists(CLI) or os.path.getmtime(CLI) < max(os.path.getmtime(LIB), os.path.getmtime(cli_src)):
-        cmd = ["g++", "-O2", "-std=c++17", "-I" + os.path.join(ROOT, "include"), cli_src, "-o", CLI, "-L" + LIBDIR,
-               "-lrray_amd", "-Wl,-rpath,$ORIGIN/../_lib"]
+    cmd = ["g++", "-O2", "-std=c++17", "-I" + os.path.join(ROOT, "include"), cli_src, "-o", CLI, "-L" + LIBDIR,
+           "-lrray_amd", "-Wl,-rpath,$ORIGIN/../_lib"]
+    cli_key = _sha([cli_src, _key_file(LIB)] + deps, "\0".join(cmd))
+    if not _key_matches(CLI, cli_key):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"cli link failed\n{r.stdout}\n{r.stderr}")
+        with open(_key_file(CLI), "w") as fh:
+            fh.write(cli_key + "\n")
     return LIB
 
 

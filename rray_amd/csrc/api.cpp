@@ -460,7 +460,11 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             A.lcount = lc + d * rr::LC_COUNT;
             if (order_ok && d == 0) {
                 A.tile_perm = c->order_valid ? c->tile_perm.as<uint32_t>() : nullptr;
-                A.tile_cost = c->tile_cost.as<uint32_t>();
+                // the waves record their costs only in a frame the sort below reads (every kRR_ORDER_EVERY-th):
+                // each record is one scattered 4-byte store per wave, a partial line that L2 writes back alone
+                // (47 MB of the C3 chain kernel's 0.55 GB of writes per frame, profiles/r05/attrib_c3.txt)
+                const bool sort_after = !c->order_valid || c->order_age + 1 >= kRR_ORDER_EVERY;
+                A.tile_cost = sort_after ? c->tile_cost.as<uint32_t>() : nullptr;
                 A.order_group = order_group;
             }
             A.counters = frame_counters(c, c->epoch);

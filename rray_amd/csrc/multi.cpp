@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -101,6 +102,8 @@ struct rr_group {
     std::vector<hipStream_t> render_st[2], comm_st;
     std::vector<hipEvent_t> ev_rendered[2], ev_gathered[2];
     bool virt = false;                    // rr_create_virtual: every part on one device, send/recv = local copies
+    int fail_after = -1;                  // fault injection for the drain tests (RRAY_TEST_FAIL_AFTER_PART): the call
+                                          // fails once this local part's render is enqueued
     hipEvent_t ev_caller = nullptr;       // root: the caller's stream position at the gather call
     std::vector<DevMem> tile[2];          // per local part: its tile (rows of the part, in tile order)
     DevMem frame;                         // root: assembled frame for the blocking rr_render
@@ -118,6 +121,7 @@ namespace rr {
 
 static int group_setup(rr_group* g) {
     const int n = (int)g->devices.size();
+    if (const char* f = std::getenv("RRAY_TEST_FAIL_AFTER_PART")) g->fail_after = std::atoi(f);
     g->comm_st.assign(n, nullptr);
     for (int b = 0; b < 2; ++b) {
         g->subs[b].assign(n, nullptr);
@@ -319,6 +323,7 @@ static int enqueue_frame(rr_group* g, const rr_camera* cam, const std::vector<rr
         enqueued = true;
         int rc = rr_render_device(g->subs[b][l], cam, &opts[l], nullptr, g->tile[b][l].p, g->render_st[b][l]);
         if (rc != RR_OK) return rc;
+        if (l == g->fail_after) return gfail(RR_E_HIP, "injected failure after part " + std::to_string(l) + "'s render");
         GHIP(hipEventRecord(g->ev_rendered[b][l], g->render_st[b][l]));
         GHIP(hipStreamWaitEvent(g->gather_stream(l), g->ev_rendered[b][l], 0));
     }

@@ -40,6 +40,25 @@ def test_library_exports_every_header_symbol(R):
     assert sorted(R._lib.EXPORTS) == names
 
 
+def test_kernel_list_matches_the_library():
+    """rr_kernel_times reports K_COUNT kernels (kernels.hpp KernelId): the Python names (_lib.KERNELS) and the
+    header's documented order and count must be that list.  The GPU test test_kernel_times_count_matches checks
+    the call's return value."""
+    from rray_amd import _lib
+
+    kh = open(os.path.join(ROOT, "rray_amd", "csrc", "kernels.hpp")).read()
+    enum = re.search(r"enum KernelId \{([^}]*)\}", kh).group(1)
+    ids = [e.strip().split("=")[0].strip() for e in enum.split(",") if e.strip()]
+    assert ids[-1] == "K_COUNT"
+    names = [i[2:].lower() for i in ids[:-1]]
+    assert names == _lib.KERNELS
+    hdr = re.sub(r"\s+", " ", re.sub(r"\n\s*\*", " ", open(os.path.join(ROOT, "include", "rray", "rray.h")).read()))
+    doc = re.search(r"per kernel in the order ([a-z0-9_, ]+) \(returns the number of kernels, (\d+);", hdr)
+    assert doc, "rr_kernel_times documentation not found"
+    assert [n.strip() for n in doc.group(1).split(",")] == _lib.KERNELS
+    assert int(doc.group(2)) == len(_lib.KERNELS)
+
+
 def test_no_cpu_fallback_without_device(R):
     if R.device_count() > 0:
         pytest.skip("a GPU is visible; the no-device path is exercised on CPU hosts")

@@ -151,3 +151,26 @@ def test_camera_inside_a_sphere(renderer, R):
     canvas, _ = o.render(ocam, max_depth=3)
     assert float(np.max(np.abs(got - o.aa_average(canvas, 1)))) <= TOL
     assert np.all(got > 0)
+
+
+def test_kernel_times_count_matches(R, renderer):
+    """rr_kernel_times returns K_COUNT = len(_lib.KERNELS) kernels (trace .. chain, deep), and a reflective scene's
+    frame is timed under `chain` (one launch per frame)."""
+    import ctypes as C
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    text = open(os.path.join(root, "scenes", "c3_s1024_reflect.yaml")).read()
+    scene = R.YamlScene(text, 32, 16, 1)
+    renderer.upload(scene)
+    renderer.kernel_profile(True)
+    try:
+        renderer.render(scene.camera, aa=1)
+        ms, n = (C.c_double * 16)(), (C.c_uint64 * 16)()
+        k = R.lib().rr_kernel_times(renderer.h, ms, n, 16)
+        assert k == len(R._lib.KERNELS)
+        times = renderer.kernel_times()
+        assert list(times) == R._lib.KERNELS
+        assert times["chain"][1] == 1 and times["chain"][0] > 0.0
+    finally:
+        renderer.kernel_profile(False)

@@ -1,12 +1,13 @@
-"""GPU tests of the multi-device contexts (rr_create_multi / rr_create_rank: row tiles received straight into
-frame order) and of the drop-in CLI end to end (main.rs:49-77 -> PNG on disk).
+"""GPU tests of the multi-device contexts (rr_create_multi / rr_create_rank: row tiles sent to rank 0 one per part,
+received into a staging buffer and placed into frame order) and of the drop-in CLI end to end
+(main.rs:49-77 -> PNG on disk).
 
 The GPU box has one MI355X, so the RCCL groups here have one device / one rank: they exercise the whole
-path through the C ABI (tile render, one RCCL group of per-run ncclSend / ncclRecv — rank 0 sends its own
-runs to itself — into the frame rows, double-buffered pipelining).  The N > 1 frame assembly runs through
+path through the C ABI (tile render, one RCCL group with the part's ncclSend to itself and rank 0's ncclRecv into
+the staging buffer, the placement kernel, double-buffered pipelining).  The N > 1 frame assembly runs through
 virtual groups (rr_create_virtual): N parts on the one device, each with its own context and streams, every
-tile's runs placed into the frame by a copy kernel with nparts = N — everything of the N > 1 path except
-the RCCL transfer between devices.
+tile copied into its staging rows at rr_stage_row_offset and placed by the same per-part kernels with nparts = N —
+everything of the N > 1 path except the ncclSend / ncclRecv pairs between devices.
 """
 import ctypes
 import os
@@ -231,3 +232,34 @@ def test_cli_multi_device_env(tmp_path):
                         env=env)
     assert r1.returncode == 0 and r2.returncode == 0, (r1.stderr, r2.stderr)
     assert np.array_equal(_png(out1), _png(out2))
+
+
+def test_failed_group_frame_drains_its_work(R, single, monkeypatch):
+    """A group call that fails after enqueuing work (fault injection: RRAY_TEST_FAIL_AFTER_PART = 0, so part 0's
+    render is in flight when part 1 fails) drains every stream before it returns the error: close() then has
+    nothing left to wait for, and a context built afterwards renders the frame bit for bit (the
+    round-4 teardown hang)."""
+    import time
+
+    W, H, aa = 48, 40, 3
+    scene = _scene(R, "c3_s1024_reflect.yaml", W, H, aa)
+    single.upload(scene)
+    ref = single.render(scene.camera, aa=aa)
+    monkeypatch.setenv("RRAY_TEST_FAIL_AFTER_PART", "0")
+    g = R.Renderer.virtual(0, 3)
+    monkeypatch.delenv("RRAY_TEST_FAIL_AFTER_PART")
+    try:
+        g.upload(scene)
+        with pytest.raises(R.RRError) as e:
+            g.render(scene.camera, aa=aa)
+        assert "injected failure" in str(e.value)
+    finally:
+        t0 = time.perf_counter()
+        g.close()
+        assert time.perf_counter() - t0 < 10.0
+    g = R.Renderer.virtual(0, 3)
+    try:
+        g.upload(scene)
+        assert np.array_equal(g.render(scene.camera, aa=aa)["avg"], ref["avg"])
+    finally:
+        g.close()
