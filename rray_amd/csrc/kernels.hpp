@@ -94,7 +94,7 @@ struct CombArgs {
 // RR_PRELIT_LIGHTS lights (PRE) every light's prelit terms ([light][6][256] doubles) and the area-light
 // stage (scenes with an area light).
 constexpr int RR_PRELIT_LIGHTS = 2;
-constexpr size_t RR_AREA_STAGE_BYTES = 3 * 256 * 8 + 2 * 256 * 4;
+constexpr size_t RR_AREA_STAGE_BYTES = 3 * 256 * 8 + 3 * 256 * 4;
 constexpr size_t RR_CHAIN_STAGE_BYTES = 10 * 256 * 8 + 3 * 256 * 4;  // chain kernels: parked ray, level-0 record, Px0
 
 // Level-0 camera events run in 8x8-sample tiles of the part-local supersampled canvas (8-row bands,
