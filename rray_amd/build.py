@@ -188,15 +188,22 @@ def build_variant(name, defines, verbose=False, patch=None):
         pre = [HIPCC, "-x", "hip"] if src.endswith(".cpp") else [HIPCC]
         inc = ["-I" + os.path.join(os.path.dirname(os.path.dirname(csrc)), "include")] if patch else []
         cmd = pre + COMMON + inc + DEVICE + UNIT_FLAGS.get(src, []) + flags + ["-c", os.path.join(csrc, src), "-o", o]
+        if src.endswith(".hip"):
+            cmd += REMARKS
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"compile failed: {src}\n{r.stderr}")
+        if src.endswith(".hip"):
+            json.dump(_resources(r.stderr), open(o + ".resources.json", "w"))
         return o
 
     with cf.ThreadPoolExecutor(min(len(SOURCES), max(1, min(16, os.cpu_count() or 1)))) as ex:
         objs = list(ex.map(one, SOURCES))
+    # experiment libraries obey the cross-lane rule too: a spilled cross-lane walk reads stale lanes (wrong loop
+    # bounds), the likeliest cause of the round-4 teardown hang on an experiment build
+    check_cross_lane([o + ".resources.json" for o in objs if os.path.exists(o + ".resources.json")])
     objs.append(_digest_object(verbose, out_dir, "variant-" + name))  # never equal to a source digest
     lib = os.path.join(out_dir, "librray_amd.so")
     r = subprocess.run([HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", lib] + objs +
