@@ -7,9 +7,9 @@ value of the multi-GPU workload (`scaling_anchor`), so the 1/2/4/8-GPU curve has
 
 N > 1: BASELINE configs[2] — the same scene at 3840x2160 AA=3, reflective, depth 5 (C3), ONE frame
 per step split across the ranks in interleaved 8-row blocks (rank r renders output rows
-{y : (y // 8) % N == r}); each rank's f64 AA-averaged tile goes to rank 0 in one RCCL gather
-(torch.distributed backend "nccl" = RCCL over xGMI), double-buffered so the gather of frame k
-overlaps the render of frame k+1 ("scaling": "strong": the frame is fixed).  After the timed region
+{y : (y // 8) % N == r}); each rank's f64 AA-averaged tile goes to rank 0 in one RCCL send (the
+library's group: one ncclSend per part, one ncclRecv per part into rank 0's staging buffer, one placement
+kernel per part), double-buffered so the transfer of frame k overlaps the render of frame k+1 ("scaling": "strong": the frame is fixed).  After the timed region
 rank 0 checks that the gathered frame is bit-identical to its own single-part render.
 `--mode frames` (opt-in) is the render-farm sharding: one whole frame per rank per step, no
 data-path collective ("scaling": "weak").
@@ -115,7 +115,7 @@ def main():
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
                     help=f"default: {SINGLE_GPU_WORKLOAD} at N=1, {MULTI_GPU_WORKLOAD} at N>1")
     ap.add_argument("--mode", choices=("frames", "tiles"), default=None,
-                    help="multi-rank sharding: row tiles of one frame + RCCL gather (default at N>1) or whole "
+                    help="multi-rank sharding: row tiles of one frame + RCCL transfer (default at N>1) or whole "
                          "frames per rank (opt-in render farm, weak scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-stride", type=int, default=None,
@@ -134,7 +134,7 @@ def main():
     ap.add_argument("--gather", choices=("abi", "torch"), default="abi",
                     help="tiles at N>1: the library's own RCCL group (rr_create_rank + rr_render_gather_device; the "
                          "torch process group only carries host-side coordination over gloo) or torch.distributed's "
-                         "RCCL gather of the tiles (rray_amd/dist.py FramePipeline)")
+                         "per-part RCCL send / receive of the tiles (rray_amd/dist.py FramePipeline)")
     ap.add_argument("--force-dist", action="store_true",
                     help="rehearsal: run the multi-rank path (RCCL process group, pipelined gather) even at 1 rank")
     ap.add_argument("--dry-run", action="store_true",
@@ -229,7 +229,7 @@ class Session:
                 self.rend = Contexts([rend] + extra)
         elif gather == "abi":
             # the library's group context splits the frame into this rank's row tile, gathers the f64
-            # tiles to rank 0 with one RCCL gather (double-buffered: frame k+1 renders while frame k is
+            # tiles to rank 0 with one RCCL send / receive per part (double-buffered: frame k+1 renders while frame k is
             # gathered) and un-interleaves them into frame_t
             if rank == 0:
                 self.frame_t = torch.zeros((self.H, self.W, 3), dtype=torch.float64, device=dev)
@@ -238,7 +238,7 @@ class Session:
             self.stream = torch.cuda.current_stream(dev)
         else:
             # f64 tiles (bit-identical to the 1-GPU image), double-buffered: rendering frame k+1 overlaps
-            # the RCCL gather of frame k
+            # the per-part RCCL transfer of frame k
             self.pipe = rdist.FramePipeline(self.H, self.W, 3, torch.float64, dev, block=BLOCK)
             self.opts = R._lib.RenderOpts(self.aa, self.depth, 0, 0, rank, world, BLOCK,
                                           R._lib.RR_OUT_AVG | R._lib.RR_NO_FRAME_TIMING)
@@ -582,8 +582,8 @@ def gpu_bench(args, world, mode, workload):
                       "note": "N=1 value of the N>1 workload (row tiles with nparts=1), for the scaling curve"}
     if rank == 0:
         via = ("library RCCL group: rr_create_rank + rr_render_gather_device" if args.gather == "abi" else
-               "torch.distributed RCCL gather")
-        par = (f"row-tiles x{world} + rccl gather (f64 tiles, pipelined; {via})" if world > 1 or sess.multi else
+               "torch.distributed RCCL isend / irecv per part")
+        par = (f"row-tiles x{world} + rccl send/recv per part (f64 tiles, pipelined; {via})" if world > 1 or sess.multi else
                "single GPU, whole frame") if tiles else \
             f"frame-parallel x{world} (one whole frame per rank per step, no data-path collective)"
         line = {"metric": METRIC, "value": round(value, 3), "unit": "Mpixel-samples/s", "n_gpus": world,
@@ -688,7 +688,7 @@ def dry_run(args, world, mode, workload):
                 "dry_run": f"gloo on CPU, CPU-oracle tiles at {W}x{H} (not {W0}x{H0}): a rehearsal, not a measurement",
                 "config": {"workload": workload, "scene": scene_file, "width": W, "height": H, "aa": aa,
                            "max_depth": depth, "frames_per_step": frames_per_step,
-                           "parallelism": (f"row-tiles x{world} + rccl gather (f64 tiles, pipelined)" if tiles else
+                           "parallelism": (f"row-tiles x{world} + per-part send/recv (f64 tiles, pipelined)" if tiles else
                                            f"frame-parallel x{world} (one whole frame per rank per step, "
                                            "no data-path collective)")},
                 "tile_identity": identity}

@@ -1,7 +1,7 @@
 // cli.cpp — `rray` drop-in CLI (src/main.rs:49-77): same flags and defaults.
 //   rray -W <width=800> -H <height=600> -s <scene.yaml> -o <output.png> -a <aa=1, max 5>
 // Renders on GPU 0 (RRAY_DEVICE=<id> picks another one); RRAY_DEVICES=<id,id,...> or RRAY_DEVICES=all
-// splits the frame over several GPUs of this host (rr_create_multi: row tiles + one RCCL gather).
+// splits the frame over several GPUs of this host (rr_create_multi: row tiles + one RCCL transfer per part).
 // No CPU fallback.
 #include <cstdio>
 #include <cstdlib>

@@ -15,9 +15,9 @@ namespace rr {
 // DESIGN.md §5).  Global ranks rank0 .. rank0 + nlocal - 1 live in this process.
 int group_create_local(int n, const int* device_ids, rr_group** out);
 int group_create_rank(int device, int nranks, int rank, const uint8_t* unique_id, rr_group** out);
-// nparts virtual ranks on one device (rr_create_virtual): the same tiles, buffers, streams and
-// un-interleave as a real group, with the gather done by device-local copies into rank 0's receive
-// buffer in ncclGather's layout
+// nparts virtual ranks on one device (rr_create_virtual): the same tiles, buffers, streams, staging buffer and
+// placement kernels as a real group, with each ncclSend / ncclRecv pair done by a device-local copy into rank 0's
+// staging buffer (partition.hpp stage_row_offset)
 int group_create_virtual(int device, int nparts, rr_group** out);
 void group_destroy(rr_group* g);
 int group_upload(rr_group* g, const rr_scene_desc* d);

@@ -305,7 +305,7 @@ class Renderer:
         return a.value, b.value, c.value
 
     def render_gather_device(self, cam, opts, d_frame, stream=None):
-        """Whole frame (row tiles over the group's devices + one RCCL gather) into d_frame on rank 0's
+        """Whole frame (row tiles over the group's devices + one RCCL send / receive per part) into d_frame on rank 0's
         device, in `stream` order (asynchronous)."""
         check(lib().rr_render_gather_device(self.h, C.byref(cam), C.byref(opts), C.c_void_p(d_frame) if d_frame else None,
                                             C.c_void_p(stream) if stream else None))
