@@ -49,11 +49,33 @@ def source_digest():
 
 
 def _dep_files():
-    """Every file a unit may include: the csrc headers and .inc files and the public header (a unit's key hashes
-    them all — a conservative include set, so no header edit can leave a stale object behind)."""
+    """Every file a unit may include: the csrc headers and .inc files and the public header."""
     files = glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(os.path.join(CSRC, "*.inc"))
     files += glob.glob(os.path.join(ROOT, "include", "rray", "*.h"))
     return sorted(files)
+
+
+_INCLUDE = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def unit_deps(path, candidates):
+    """The project files `path` includes, transitively (quoted #include lines resolved against the including file's
+    directory).  Any quoted include that does not resolve to one of `candidates` makes the unit depend on all of
+    them, so a key can only be conservative, never stale."""
+    cand = {os.path.realpath(c) for c in candidates}
+    seen, todo = set(), [os.path.realpath(path)]
+    while todo:
+        f = todo.pop()
+        with open(f) as fh:
+            text = fh.read()
+        for inc in _INCLUDE.findall(text):
+            q = os.path.realpath(os.path.join(os.path.dirname(f), inc))
+            if q not in cand:
+                return sorted(candidates)
+            if q not in seen:
+                seen.add(q)
+                todo.append(q)
+    return sorted(c for c in candidates if os.path.realpath(c) in seen)
 
 
 def _sha(paths, extra=""):
@@ -144,7 +166,7 @@ def _compile(src, deps, verbose):
         cmd = [HIPCC, "-x", "hip"] + COMMON + DEVICE + ["-c", path, "-o", out]
     else:
         cmd += REMARKS
-    key = unit_key(path, deps, cmd)
+    key = unit_key(path, unit_deps(path, deps), cmd)
     if _key_matches(out, key) and (src.endswith(".cpp") or os.path.exists(out + ".resources.json")):
         return out
     if os.path.exists(_key_file(out)):
@@ -260,7 +282,7 @@ def build(verbose=False, jobs=None):
     cli_src = os.path.join(CSRC, "cli.cpp")
     cmd = ["g++", "-O2", "-std=c++17", "-I" + os.path.join(ROOT, "include"), cli_src, "-o", CLI, "-L" + LIBDIR,
            "-lrray_amd", "-Wl,-rpath,$ORIGIN/../_lib"]
-    cli_key = _sha([cli_src, _key_file(LIB)] + deps, "\0".join(cmd))
+    cli_key = _sha([cli_src, _key_file(LIB)] + unit_deps(cli_src, deps), "\0".join(cmd))
     if not _key_matches(CLI, cli_key):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:

@@ -101,4 +101,24 @@ def test_in_tree_objects_carry_keys_of_the_current_sources():
             cmd = [B.HIPCC, "-x", "hip"] + B.COMMON + B.DEVICE + ["-c", path, "-o", out]
         else:
             cmd = [B.HIPCC] + B.COMMON + B.DEVICE + B.UNIT_FLAGS.get(src, []) + ["-c", path, "-o", out] + B.REMARKS
-        assert B._key_matches(out, B.unit_key(path, deps, cmd)), src
+        assert B._key_matches(out, B.unit_key(path, B.unit_deps(path, deps), cmd)), src
+
+
+def test_unit_deps_follow_includes(tmp_path):
+    """A unit depends on what it includes, transitively; an include the scan cannot resolve makes it depend on every
+    candidate (conservative)."""
+    (tmp_path / "a.hpp").write_text('#include "b.inc"\n')
+    (tmp_path / "b.inc").write_text("// leaf\n")
+    (tmp_path / "c.hpp").write_text("// unrelated\n")
+    u = tmp_path / "u.cpp"
+    u.write_text('#include "a.hpp"\n#include <vector>\n')
+    cands = [str(tmp_path / n) for n in ("a.hpp", "b.inc", "c.hpp")]
+    assert B.unit_deps(str(u), cands) == sorted(cands[:2])
+    u.write_text('#include "a.hpp"\n#include "missing.hpp"\n')
+    assert B.unit_deps(str(u), cands) == sorted(cands)
+    # the product: the chain units depend on the device code, the PNG writer does not
+    deps = B._dep_files()
+    chain = B.unit_deps(os.path.join(B.CSRC, "render_chain_g0_gl.hip"), deps)
+    assert any(d.endswith("device_core.inc") for d in chain)
+    png = B.unit_deps(os.path.join(B.CSRC, "png.cpp"), deps)
+    assert not any(d.endswith("device_core.inc") for d in png)
