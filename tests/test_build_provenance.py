@@ -23,7 +23,7 @@ def tree(tmp_path, monkeypatch):
     monkeypatch.setattr(B, "CSRC", str(csrc))
     monkeypatch.setattr(B, "OBJ", str(obj))
     monkeypatch.setattr(B, "HIPCC", str(cc))
-    (csrc / "unit.cpp").write_text("int f() { return 1; }\n")
+    (csrc / "unit.cpp").write_text('#include "dep.hpp"\nint f() { return 1; }\n')
     (csrc / "dep.hpp").write_text("// header v1\n")
     return csrc, obj, log
 
@@ -48,12 +48,12 @@ def test_edit_with_an_old_mtime_still_recompiles(tree):
     deps = [str(csrc / "dep.hpp")]
     out = B._compile("unit.cpp", deps, False)
     src = csrc / "unit.cpp"
-    src.write_text("int f() { return 2; }\n")
+    src.write_text('#include "dep.hpp"\nint f() { return 2; }\n')
     os.utime(src, (1_000_000, 1_000_000))  # 1970: far older than the object
     assert os.path.getmtime(src) < os.path.getmtime(out)
     B._compile("unit.cpp", deps, False)
     assert _calls(log) == 2
-    assert open(out).read() == "int f() { return 2; }\n"
+    assert open(out).read() == '#include "dep.hpp"\nint f() { return 2; }\n'
 
 
 def test_header_edit_with_an_old_mtime_recompiles(tree):
