@@ -1,5 +1,6 @@
-// png.cpp — minimal RGBA8 PNG encoder over zlib (filter 0 per row; lossless, so decoded pixels
-// equal the reference's image-crate output).
+// png.cpp — RGBA8 PNG encoder over zlib (filter 0 per row; lossless, so decoded pixels
+// equal the reference's image-crate output), and the texture reader (texture.rs:15-19: image::open + to_rgba8):
+// PNG of every colour type, bit depth and interlace method, JPEG through jpeg.cpp.
 #include "png.hpp"
 
 #include <zlib.h>
@@ -88,18 +89,41 @@ int read_image_rgba(const std::string& path, std::vector<uint8_t>& rgba, uint32_
         return RR_E_IO;
     }
     const int channels = ctype == 0 ? 1 : ctype == 2 ? 3 : ctype == 3 ? 1 : ctype == 4 ? 2 : ctype == 6 ? 4 : 0;
-    const bool sub8 = depth < 8 && (ctype == 0 || ctype == 3);
-    if (channels == 0 || interlace != 0 || !(depth == 8 || (sub8 && (depth == 1 || depth == 2 || depth == 4)))) {
-        err = path + ": PNG layout outside the texture decoder (16-bit or interlaced)";
-        return RR_E_LIMIT;
+    const bool depth_ok = ctype == 0   ? (depth == 1 || depth == 2 || depth == 4 || depth == 8 || depth == 16)
+                          : ctype == 3 ? (depth == 1 || depth == 2 || depth == 4 || depth == 8)
+                                       : (depth == 8 || depth == 16);
+    if (channels == 0 || !depth_ok || interlace > 1) {
+        err = path + ": PNG layout outside the PNG specification (color type / bit depth / interlace method)";
+        return RR_E_IO;
     }
     if (ctype == 3 && plte.size() < 3) {
         err = path + ": palette PNG without PLTE";
         return RR_E_IO;
     }
-    const size_t stride = ((size_t)w * channels * depth + 7) / 8;
+    if ((uint64_t)w * h > (1ull << 28)) {
+        err = path + ": texture larger than 2^28 texels";
+        return RR_E_LIMIT;
+    }
+    // the sub-images: the whole image, or Adam7's seven passes (x0, y0, dx, dy), each filtered separately
+    struct Pass {
+        uint32_t x0, y0, dx, dy, pw, ph;
+    };
+    static const uint32_t adam7[7][4] = {{0, 0, 8, 8}, {4, 0, 8, 8}, {0, 4, 4, 8}, {2, 0, 4, 4},
+                                         {0, 2, 2, 4}, {1, 0, 2, 2}, {0, 1, 1, 2}};
+    std::vector<Pass> passes;
+    if (interlace == 0) {
+        passes.push_back({0, 0, 1, 1, w, h});
+    } else {
+        for (const auto& q : adam7) {
+            const uint32_t pw = w > q[0] ? (w - q[0] + q[2] - 1) / q[2] : 0, ph = h > q[1] ? (h - q[1] + q[3] - 1) / q[3] : 0;
+            if (pw && ph) passes.push_back({q[0], q[1], q[2], q[3], pw, ph});
+        }
+    }
+    const auto stride_of = [&](uint32_t pw) { return ((size_t)pw * channels * depth + 7) / 8; };
+    size_t total = 0;
+    for (const Pass& ps : passes) total += (stride_of(ps.pw) + 1) * ps.ph;
     const size_t bpp = std::max<size_t>(1, (size_t)channels * depth / 8);
-    std::vector<uint8_t> raw((stride + 1) * h);
+    std::vector<uint8_t> raw(total);
     z_stream zs{};
     if (inflateInit(&zs) != Z_OK) {
         err = "zlib init failed";
@@ -115,32 +139,40 @@ int read_image_rgba(const std::string& path, std::vector<uint8_t>& rgba, uint32_
         err = path + ": corrupt PNG image data";
         return RR_E_IO;
     }
-    // unfilter in place (filter types 0-4)
-    std::vector<uint8_t> prev(stride, 0);
-    for (uint32_t y = 0; y < h; ++y) {
-        uint8_t* row = &raw[(size_t)y * (stride + 1)];
-        uint8_t ft = row[0];
-        uint8_t* cur = row + 1;
-        for (size_t i = 0; i < stride; ++i) {
-            int a = i >= bpp ? cur[i - bpp] : 0, b = prev[i], c = i >= bpp ? prev[i - bpp] : 0;
-            int pred = ft == 0 ? 0 : ft == 1 ? a : ft == 2 ? b : ft == 3 ? (a + b) / 2 : ft == 4 ? paeth(a, b, c) : -1;
-            if (pred < 0) {
-                err = path + ": bad PNG filter type";
-                return RR_E_IO;
-            }
-            cur[i] = (uint8_t)(cur[i] + pred);
-        }
-        std::memcpy(prev.data(), cur, stride);
-    }
+    // a sample of `depth` bits at sample index k of an unfiltered row -> 8 bits, as the image crate's to_rgba8 gives it:
+    // sub-byte grey scaled by 255 / (2^depth - 1); 16-bit by FromPrimitive<u16> for u8, round(c * 255 / 65535) =
+    // (c + 128) / 257 (image 0.25 color.rs; not vendored: no reference-held 16-bit PNG pins it)
+    const auto sample8 = [&](const uint8_t* row, size_t k) -> uint8_t {
+        if (depth == 8) return row[k];
+        if (depth == 16) return (uint8_t)((((uint32_t)row[2 * k] << 8 | row[2 * k + 1]) + 128u) / 257u);
+        const size_t bit = k * (size_t)depth;
+        const int v = (row[bit / 8] >> (8 - depth - (int)(bit % 8))) & ((1 << depth) - 1);
+        return ctype == 3 ? (uint8_t)v : (uint8_t)(v * 255 / ((1 << depth) - 1));
+    };
     rgba.assign((size_t)w * h * 4, 255);
-    for (uint32_t y = 0; y < h; ++y) {
-        const uint8_t* cur = &raw[(size_t)y * (stride + 1) + 1];
-        for (uint32_t x = 0; x < w; ++x) {
-            uint8_t* o = &rgba[4 * ((size_t)y * w + x)];
-            if (sub8 || ctype == 3) {
-                size_t bit = (size_t)x * depth;
-                int v = (cur[bit / 8] >> (8 - depth - (int)(bit % 8))) & ((1 << depth) - 1);
+    size_t off = 0;
+    for (const Pass& ps : passes) {
+        const size_t stride = stride_of(ps.pw);
+        std::vector<uint8_t> prev(stride, 0);
+        for (uint32_t y = 0; y < ps.ph; ++y) {  // unfilter in place (filter types 0-4; the previous row of this pass)
+            uint8_t* row = &raw[off + (size_t)y * (stride + 1)];
+            const uint8_t ft = row[0];
+            uint8_t* cur = row + 1;
+            for (size_t i = 0; i < stride; ++i) {
+                int a = i >= bpp ? cur[i - bpp] : 0, b = prev[i], c = i >= bpp ? prev[i - bpp] : 0;
+                int pred = ft == 0 ? 0 : ft == 1 ? a : ft == 2 ? b : ft == 3 ? (a + b) / 2 : ft == 4 ? paeth(a, b, c) : -1;
+                if (pred < 0) {
+                    err = path + ": bad PNG filter type";
+                    return RR_E_IO;
+                }
+                cur[i] = (uint8_t)(cur[i] + pred);
+            }
+            std::memcpy(prev.data(), cur, stride);
+            for (uint32_t x = 0; x < ps.pw; ++x) {
+                uint8_t* o = &rgba[4 * ((size_t)(ps.y0 + y * ps.dy) * w + ps.x0 + (size_t)x * ps.dx)];
+                const size_t k = (size_t)x * channels;
                 if (ctype == 3) {
+                    const int v = sample8(cur, k);
                     if (3 * (size_t)v + 2 >= plte.size()) {
                         err = path + ": palette index out of range";
                         return RR_E_IO;
@@ -148,20 +180,22 @@ int read_image_rgba(const std::string& path, std::vector<uint8_t>& rgba, uint32_
                     o[0] = plte[3 * v];
                     o[1] = plte[3 * v + 1];
                     o[2] = plte[3 * v + 2];
-                } else {  // grey scaled to 8 bits
-                    uint8_t g = (uint8_t)(v * 255 / ((1 << depth) - 1));
-                    o[0] = o[1] = o[2] = g;
+                    continue;
                 }
-                continue;
-            }
-            const uint8_t* p = cur + (size_t)x * channels;
-            switch (ctype) {
-                case 0: o[0] = o[1] = o[2] = p[0]; break;
-                case 4: o[0] = o[1] = o[2] = p[0]; o[3] = p[1]; break;
-                case 2: o[0] = p[0]; o[1] = p[1]; o[2] = p[2]; break;
-                default: o[0] = p[0]; o[1] = p[1]; o[2] = p[2]; o[3] = p[3]; break;
+                switch (ctype) {
+                    case 0: o[0] = o[1] = o[2] = sample8(cur, k); break;
+                    case 4: o[0] = o[1] = o[2] = sample8(cur, k); o[3] = sample8(cur, k + 1); break;
+                    case 2: o[0] = sample8(cur, k); o[1] = sample8(cur, k + 1); o[2] = sample8(cur, k + 2); break;
+                    default:
+                        o[0] = sample8(cur, k);
+                        o[1] = sample8(cur, k + 1);
+                        o[2] = sample8(cur, k + 2);
+                        o[3] = sample8(cur, k + 3);
+                        break;
+                }
             }
         }
+        off += (stride + 1) * ps.ph;
     }
     width = w;
     height = h;
