@@ -30,7 +30,8 @@ CHAIN_UNITS = [f"render_chain_g{g}_{lc}.hip" for g in (2, 1, 0) for lc in ("lds"
 # per-unit flags: the chain kernels' loop must not get loop-invariant constants hoisted into registers (they
 # spill instead of being rematerialised)
 UNIT_FLAGS = {u: ["-mllvm", "-disable-machine-licm"] for u in CHAIN_UNITS}
-SOURCES = LEVEL_UNITS + CHAIN_UNITS + ["render.hip", "api.cpp", "multi.cpp", "flatten.cpp", "frontend.cpp", "yaml.cpp", "png.cpp", "jpeg.cpp"]
+SOURCES = LEVEL_UNITS + CHAIN_UNITS + ["render.hip", "api.cpp", "multi.cpp", "flatten.cpp", "frontend.cpp", "yaml.cpp", "png.cpp", "jpeg.cpp",
+                                         "imgfmt.cpp"]
 
 
 def source_digest():

@@ -1,11 +1,13 @@
 // png.cpp — RGBA8 PNG encoder over zlib (filter 0 per row; lossless, so decoded pixels
 // equal the reference's image-crate output), and the texture reader (texture.rs:15-19: image::open + to_rgba8):
-// PNG of every colour type, bit depth and interlace method, JPEG through jpeg.cpp.
+// PNG of every colour type, bit depth and interlace method; JPEG through jpeg.cpp; BMP / TGA / PNM / GIF through
+// imgfmt.cpp.
 #include "png.hpp"
 
 #include <zlib.h>
 
 #include <algorithm>
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -54,9 +56,32 @@ int read_image_rgba(const std::string& path, std::vector<uint8_t>& rgba, uint32_
         if (rc != RR_OK) err = path + ": " + err;
         return rc;
     }
+    // the other formats by signature (TGA has none: by extension, as image::open chooses every format)
+    int (*other)(const uint8_t*, size_t, std::vector<uint8_t>&, uint32_t&, uint32_t&, std::string&) = nullptr;
+    const auto ext_is = [&](const char* e) {
+        const size_t k = std::strlen(e);
+        if (path.size() < k) return false;
+        for (size_t i = 0; i < k; ++i)
+            if (std::tolower((unsigned char)path[path.size() - k + i]) != e[i]) return false;
+        return true;
+    };
+    if (file.size() >= 2 && file[0] == 'B' && file[1] == 'M')
+        other = decode_bmp_rgba;
+    else if (file.size() >= 4 && std::memcmp(file.data(), "GIF8", 4) == 0)
+        other = decode_gif_rgba;
+    else if (file.size() >= 2 && file[0] == 'P' && file[1] >= '1' && file[1] <= '6')
+        other = decode_pnm_rgba;
+    else if (ext_is(".tga"))
+        other = decode_tga_rgba;
+    if (other) {
+        int rc = other(file.data(), file.size(), rgba, width, height, err);
+        if (rc != RR_OK) err = path + ": " + err;
+        return rc;
+    }
     static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
     if (file.size() < 8 || std::memcmp(file.data(), sig, 8) != 0) {
-        err = path + ": neither PNG nor JPEG (other image formats need a host-side decoder: pass texels in rr_scene_desc)";
+        err = path + ": not PNG, JPEG, BMP, GIF, PNM or TGA (other image formats need a host-side decoder: pass texels in "
+                     "rr_scene_desc)";
         return RR_E_LIMIT;
     }
     uint32_t w = 0, h = 0;

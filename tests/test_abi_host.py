@@ -341,6 +341,118 @@ def test_png_interlaced_and_16bit_textures(R, tmp_path):
         assert np.array_equal(got, want), name
 
 
+def test_other_texture_formats_match_pil(R, tmp_path):
+    """BMP (1 / 4 / 8-bit palette, 24-bit, 32-bit bitfields, top-down), TGA (grey, RGB, RGBA, colour-mapped, raw and
+    run-length, both origins), PNM (P1-P6) and GIF (plain and interlaced) — the formats image::open decodes with its
+    default features (texture.rs:15-19) — decoded by the product front-end equal PIL's decoding of the same files."""
+    from PIL import Image
+
+    rng = np.random.default_rng(5)
+
+    def rgb(h, w):
+        return Image.fromarray(rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8), "RGB")
+
+    files = []
+
+    def add(name, img, **kw):
+        img.save(tmp_path / name, **kw)
+        files.append(name)
+
+    add("a.bmp", rgb(13, 17))
+    add("b.bmp", rgb(9, 6).convert("P", palette=Image.ADAPTIVE, colors=200))
+    add("c.bmp", rgb(7, 11).convert("1"))
+    add("d.bmp", rgb(5, 9).convert("L"))
+    add("e.bmp", Image.fromarray(rng.integers(0, 256, size=(6, 7, 4), dtype=np.uint8), "RGBA"))
+    add("f.tga", rgb(10, 12))
+    add("g.tga", rgb(10, 12), compression="tga_rle")
+    add("h.tga", Image.fromarray(rng.integers(0, 256, size=(5, 8, 4), dtype=np.uint8), "RGBA"), compression="tga_rle")
+    add("i.tga", rgb(7, 5).convert("L"))
+    add("j.tga", rgb(7, 5).convert("P", palette=Image.ADAPTIVE, colors=64))
+    add("k.tga", rgb(6, 9), orientation=1)
+    add("l.ppm", rgb(8, 11))
+    add("m.pgm", rgb(8, 11).convert("L"))
+    add("n.pbm", rgb(9, 13).convert("1"))
+    add("o.gif", rgb(12, 14))
+    add("p.gif", rgb(19, 23), interlace=True)
+    add("q.gif", Image.fromarray(np.tile(np.arange(250, dtype=np.uint8), (40, 1)), "L"))
+    # the ASCII PNM variants (PIL writes binary ones) and a 4-bit palette BMP, by hand
+    a = rng.integers(0, 256, size=(3, 4, 3))
+    (tmp_path / "r.ppm").write_text("P3\n# comment\n4 3\n255\n" + " ".join(str(int(v)) for v in a.reshape(-1)) + "\n")
+    g = rng.integers(0, 256, size=(3, 5))
+    (tmp_path / "s.pgm").write_text("P2 5 3 255\n" + "\n".join(" ".join(str(int(v)) for v in r) for r in g) + "\n")
+    b = rng.integers(0, 2, size=(2, 9))
+    (tmp_path / "t.pbm").write_text("P1\n9 2\n" + "\n".join("".join(str(int(v)) for v in r) for r in b) + "\n")
+    files += ["r.ppm", "s.pgm", "t.pbm"]
+    scene = "".join(f"  - type: sphere\n    material: {{pattern: {{type: image, file: '{f}'}}}}\n" for f in files)
+    text = ("camera: {fov: 60, from: [0, 0, -5], to: [0, 0, 0], up: [0, 1, 0]}\nlights:\n  - type: point\n"
+            "    color: [1, 1, 1]\n    position: [0, 0, -5]\nscene:\n" + scene)
+    scn = R.YamlScene(text, 8, 8, 1, obj_root=str(tmp_path))
+    d = scn.desc()
+    assert d.n_textures == len(files)
+    off = 0
+    for i, f in enumerate(files):
+        w, h = d.tex_size[2 * i], d.tex_size[2 * i + 1]
+        got = np.ctypeslib.as_array(d.texels, shape=(off + w * h * 4,))[off:].reshape(h, w, 4)[..., :3]
+        off += w * h * 4
+        ref = np.asarray(Image.open(tmp_path / f).convert("RGB"))
+        assert got.shape == ref.shape, f
+        assert np.array_equal(got, ref), f
+    with pytest.raises(R.RRError) as e:  # an unknown format is refused, not misread
+        (tmp_path / "u.xyz").write_bytes(b"\x00\x01garbage")
+        R.YamlScene(text.replace("'a.bmp'", "'u.xyz'"), 8, 8, 1, obj_root=str(tmp_path))
+    assert e.value.code == R._lib.RR_E_LIMIT
+
+
+def test_corrupt_textures_under_asan(tmp_path):
+    """The texture reader (png.cpp, jpeg.cpp, imgfmt.cpp: host code) built with g++ -fsanitize=address, on files of
+    every format truncated at random points and with random bytes flipped: each is decoded or refused with an error
+    code, with no out-of-bounds access reported (and a decoded image always holds width x height texels)."""
+    import shutil
+    import subprocess
+
+    from PIL import Image
+
+    if not shutil.which("g++"):
+        pytest.skip("no g++")
+    exe = str(tmp_path / "img_asan")
+    csrc = os.path.join(ROOT, "rray_amd", "csrc")
+    r = subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address", "-fno-omit-frame-pointer",
+                        "-I" + os.path.join(ROOT, "include"), os.path.join(ROOT, "tools", "asan_image_main.cpp"),
+                        os.path.join(csrc, "png.cpp"), os.path.join(csrc, "jpeg.cpp"), os.path.join(csrc, "imgfmt.cpp"),
+                        "-lz", "-o", exe], capture_output=True, text=True)
+    if r.returncode != 0 and "sanitize" in r.stderr:
+        pytest.skip("AddressSanitizer unavailable")
+    assert r.returncode == 0, r.stderr
+    rng = np.random.default_rng(17)
+    img = Image.fromarray(rng.integers(0, 256, size=(13, 11, 3), dtype=np.uint8), "RGB")
+    seeds = []
+    for name, kw in (("s.png", {}), ("s.jpg", {"quality": 80}), ("s.bmp", {}), ("s.tga", {"compression": "tga_rle"}),
+                     ("s.ppm", {}), ("s.gif", {"interlace": True})):
+        img.save(tmp_path / name, **kw)
+        seeds.append(tmp_path / name)
+    img.convert("P", palette=Image.ADAPTIVE, colors=16).save(tmp_path / "p.bmp")
+    seeds.append(tmp_path / "p.bmp")
+    files = []
+    for sd in seeds:
+        data = bytearray(sd.read_bytes())
+        for k in range(24):
+            m = bytearray(data)
+            if k % 3 == 0:
+                m = m[: int(rng.integers(1, len(m)))]
+            else:
+                for _ in range(1 + k % 5):
+                    m[int(rng.integers(0, len(m)))] = int(rng.integers(0, 256))
+            f = tmp_path / f"{sd.stem}_{k}{sd.suffix}"
+            f.write_bytes(bytes(m))
+            files.append(str(f))
+    r = subprocess.run([exe] + [str(s) for s in seeds] + files, capture_output=True, text=True,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    rcs = [int(line.split()[0]) for line in r.stdout.splitlines()]
+    assert len(rcs) == len(seeds) + len(files)
+    assert rcs[: len(seeds)] == [0] * len(seeds)  # the intact files decode
+
+
 def test_group_contexts_need_a_device(R):
     """rr_create_multi / rr_create_rank validate their arguments and, like rr_create, have no CPU
     fallback (the multi-GPU path itself runs in tests/test_gpu_multi.py)."""
