@@ -249,62 +249,13 @@ def test_png_texture_decoder_matches_pil(R):
     assert e.value.code == R._lib.RR_E_LIMIT
 
 
-def _png_bytes(img, ctype, depth, interlace, palette=None):
-    """A PNG file built here (zlib, filter types cycling 0-4 per row, optional Adam7 passes): img is (h, w, c) of
-    sample values (uint8 or uint16)."""
-    import struct
-    import zlib
-
-    h, w = img.shape[:2]
-    ch = img.shape[2]
-
-    def pack(sub):
-        rows = []
-        bpp = max(1, ch * depth // 8)
-        prev = bytes((sub.shape[1] * ch * depth + 7) // 8)
-        for y in range(sub.shape[0]):
-            if depth == 16:
-                line = sub[y].astype(">u2").tobytes()
-            elif depth == 8:
-                line = sub[y].astype(np.uint8).tobytes()
-            else:
-                bits = "".join(format(int(v), f"0{depth}b") for v in sub[y].reshape(-1))
-                bits += "0" * (-len(bits) % 8)
-                line = bytes(int(bits[i:i + 8], 2) for i in range(0, len(bits), 8))
-            ft = y % 5
-            out = bytearray([ft])
-            for i, v in enumerate(line):
-                a = line[i - bpp] if i >= bpp else 0
-                b = prev[i]
-                c = prev[i - bpp] if i >= bpp else 0
-                p0 = a + b - c
-                pa, pb, pc = abs(p0 - a), abs(p0 - b), abs(p0 - c)
-                paeth = a if pa <= pb and pa <= pc else (b if pb <= pc else c)
-                out.append((v - (0, a, b, (a + b) // 2, paeth)[ft]) & 255)
-            rows.append(bytes(out))
-            prev = line
-        return b"".join(rows)
-
-    if interlace:
-        passes = [(0, 0, 8, 8), (4, 0, 8, 8), (0, 4, 4, 8), (2, 0, 4, 4), (0, 2, 2, 4), (1, 0, 2, 2), (0, 1, 1, 2)]
-        data = b"".join(pack(img[y0::dy, x0::dx]) for x0, y0, dx, dy in passes if img[y0::dy, x0::dx].size)
-    else:
-        data = pack(img)
-
-    def chunk(t, d):
-        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xFFFFFFFF)
-
-    png = b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, interlace))
-    if palette is not None:
-        png += chunk(b"PLTE", bytes(palette))
-    return png + chunk(b"IDAT", zlib.compress(data, 6)) + chunk(b"IEND", b"")
-
-
 def test_png_interlaced_and_16bit_textures(R, tmp_path):
     """Adam7-interlaced PNGs (every colour type and bit depth the image crate decodes) equal PIL's decoding; 16-bit
     samples become 8 bits as image's to_rgba8 converts them, round(c * 255 / 65535) = (c + 128) / 257 (image 0.25
     FromPrimitive<u16> for u8; parity unpinned: no reference-held 16-bit PNG, and PIL truncates instead)."""
     from PIL import Image
+
+    from png_helpers import png_bytes
 
     rng = np.random.default_rng(11)
     cases = []
@@ -316,7 +267,7 @@ def test_png_interlaced_and_16bit_textures(R, tmp_path):
             img = rng.integers(0, hi + 1, size=(h, w, ch)).astype(np.uint16 if depth == 16 else np.uint8)
             pal = rng.integers(0, 256, size=3 * (1 << depth)).tolist() if ctype == 3 else None
             name = f"t_{ctype}_{depth}_{interlace}.png"
-            (tmp_path / name).write_bytes(_png_bytes(img, ctype, depth, interlace, pal))
+            (tmp_path / name).write_bytes(png_bytes(img, ctype, depth, interlace, pal))
             cases.append((name, ctype, depth, img, pal))
     scene = "".join(f"  - type: sphere\n    material: {{pattern: {{type: image, file: '{c[0]}'}}}}\n" for c in cases)
     text = ("camera: {fov: 60, from: [0, 0, -5], to: [0, 0, 0], up: [0, 1, 0]}\nlights:\n  - type: point\n"

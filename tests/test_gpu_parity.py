@@ -649,3 +649,43 @@ def test_area_light_png_statistically(renderer, R):
     assert stable.sum() > 300000
     assert (d > 0).sum() <= 0.001 * d.size and d.max() <= 2
     assert inside.mean() >= 0.995 and mean_dev < 1.0
+
+
+def test_texture_formats_through_gpu(renderer, tmp_path):
+    """Spheres textured from BMP, GIF (interlaced), TGA (run-length), PNM and interlaced PNG files (texture.rs:15-19,
+    sphere uv mapping): decoded by the product front-end (png.cpp, imgfmt.cpp) on one side and by PIL in the oracle on
+    the other, rendered on the GPU and in the oracle — the frames are bit-identical, with equal recursion counters."""
+    from PIL import Image
+
+    import rray_amd as R
+    from oracle.scene_yaml import build_from_yaml
+
+    rng = np.random.default_rng(23)
+    ys, xs = np.mgrid[0:32, 0:64]
+    base = np.stack([(xs * 4) % 256, (ys * 8) % 256, ((xs + ys) * 3) % 256], -1).astype(np.uint8)
+    base ^= rng.integers(0, 32, size=base.shape, dtype=np.uint8)
+    img = Image.fromarray(base, "RGB")
+    img.save(tmp_path / "t.bmp")
+    img.save(tmp_path / "t.gif", interlace=True)
+    img.save(tmp_path / "t.tga", compression="tga_rle")
+    img.save(tmp_path / "t.ppm")
+    from png_helpers import png_bytes
+
+    (tmp_path / "t.png").write_bytes(png_bytes(base, 2, 8, 1))
+    files = ["t.bmp", "t.gif", "t.tga", "t.ppm", "t.png"]
+    objs = "".join(
+        f"  - type: sphere\n    transforms:\n      - type: scale\n        amount: [0.45, 0.45, 0.45]\n"
+        f"      - type: translate\n        amount: [{-2.0 + k}, 1, 0]\n"
+        f"    material:\n      pattern: {{type: image, file: '{f}'}}\n      specular: 0.3\n"
+        for k, f in enumerate(files))
+    text = ("camera: {fov: 60, from: [0, 1.5, -5], to: [0, 1, 0], up: [0, 1, 0]}\nlights:\n  - type: point\n"
+            "    color: [1, 1, 1]\n    position: [-10, 10, -10]\nscene:\n" + objs)
+    W, H, aa = 96, 48, 2
+    scene = R.YamlScene(text, W, H, aa, obj_root=str(tmp_path))
+    o, cam = build_from_yaml(text, W, H, aa, obj_root=str(tmp_path))
+    renderer.upload(scene)
+    got = renderer.render(scene.camera, aa=aa, max_depth=5, canvas=True)
+    canvas, st = o.render(cam, max_depth=5)
+    _, exact = _compare(got["canvas"], canvas, "texture formats canvas")
+    assert exact == 1.0
+    assert got["stats"]["shade_events"] == st["shade_events"]
