@@ -184,11 +184,12 @@ def _compile(src, deps, verbose):
     return out
 
 
-def build_variant(name, defines, verbose=False, patch=None):
+def build_variant(name, defines, verbose=False, patch=None, extra=None):
     """Experiment build into abtest/<name>/librray_amd.so; select it at run time with RRAY_EXPERIMENT=1
     RRAY_LIB=<path>.  Never used by the product path.  patch: a unified diff (tools/patches/*.patch,
     paths relative to the repo root) applied to a copy of the sources (experiment code such as per-wave
-    phase timers lives there, not in the product sources); defines: extra -D flags."""
+    phase timers lives there, not in the product sources); defines: extra -D flags; extra: extra compiler flags
+    for the device units (.hip), e.g. a scheduler strategy."""
     import shutil
 
     out_dir = os.path.join(ROOT, "abtest", name)  # travels to the GPU box (abtest/ is git-ignored)
@@ -212,7 +213,7 @@ def build_variant(name, defines, verbose=False, patch=None):
         inc = ["-I" + os.path.join(os.path.dirname(os.path.dirname(csrc)), "include")] if patch else []
         cmd = pre + COMMON + inc + DEVICE + UNIT_FLAGS.get(src, []) + flags + ["-c", os.path.join(csrc, src), "-o", o]
         if src.endswith(".hip"):
-            cmd += REMARKS
+            cmd += REMARKS + list(extra or [])
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -294,11 +295,15 @@ def build(verbose=False, jobs=None):
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 2 and sys.argv[1] == "variant":  # variant <name> [--patch file] [DEFINE ...]
+    if len(sys.argv) > 2 and sys.argv[1] == "variant":  # variant <name> [--patch file] [--flags "..."] [DEFINE ...]
         args = sys.argv[3:]
-        patch = None
-        if args[:1] == ["--patch"]:
-            patch, args = args[1], args[2:]
-        print(build_variant(sys.argv[2], args, patch=patch))
+        patch, extra = None, None
+        while args[:1] in (["--patch"], ["--flags"]):
+            if args[0] == "--patch":
+                patch = args[1]
+            else:
+                extra = args[1].split()
+            args = args[2:]
+        print(build_variant(sys.argv[2], args, patch=patch, extra=extra))
     else:
         print(build(verbose="-v" in sys.argv))
