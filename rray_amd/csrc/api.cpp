@@ -16,6 +16,7 @@
 #include "kernels.hpp"
 #include "multi.hpp"
 #include "partition.hpp"
+#include "trace.hpp"
 #include "rr_math.hpp"
 
 namespace {
@@ -720,7 +721,9 @@ void rr_destroy(rr_ctx* c) {
         return;
     }
     (void)hipSetDevice(c->device);
+    rr::trace("rr_destroy %p: synchronise", (void*)c);
     if (c->stream) (void)sync_ctx(c);
+    rr::trace("rr_destroy %p: free", (void*)c);
     for (DBuf* b : {&c->culls, &c->chunks, &c->nodes, &c->groups, &c->shapes, &c->tris, &c->mats, &c->pats, &c->lights, &c->textures, &c->texels, &c->counters,
                     &c->lcount, &c->hit, &c->n12, &c->n1n2, &c->ev_a, &c->ev_b, &c->canvas, &c->rays0, &c->qout, &c->tiles,
                     &c->tile_cost, &c->tile_perm, &c->tile_hist, &c->deep, &c->deep_count})
@@ -738,6 +741,7 @@ void rr_destroy(rr_ctx* c) {
     for (hipEvent_t e : c->pass_ev) (void)hipEventDestroy(e);
     if (c->aa_stream) (void)hipStreamDestroy(c->aa_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    rr::trace("rr_destroy %p: done", (void*)c);
     delete c;
 }
 

@@ -33,6 +33,7 @@
 #include "device_guard.hpp"
 #include "kernels.hpp"
 #include "partition.hpp"
+#include "trace.hpp"
 
 void rr_set_error(const char* msg);  // api.cpp
 
@@ -245,10 +246,14 @@ static void drain_stream(hipStream_t st, const char* what, size_t part, int set)
     bool told = false;
     for (;;) {
         const hipError_t e = hipStreamQuery(st);
-        if (e != hipErrorNotReady) return;  // done, or failed (then nothing more completes on it)
+        if (e != hipErrorNotReady) {  // done, or failed (then nothing more completes on it)
+            if (e != hipSuccess) trace("drain: %s stream of part %zu (set %d): %s", what, part, set, hipGetErrorString(e));
+            return;
+        }
         if (!told && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
             std::fprintf(stderr, "rray: group teardown: %s stream of part %zu (set %d) still busy after 30 s\n", what,
                          part, set);
+            trace("drain: %s stream of part %zu (set %d) still busy after 30 s", what, part, set);
             told = true;
         }
         std::this_thread::sleep_for(std::chrono::microseconds(200));
@@ -268,9 +273,21 @@ static void group_drain(rr_group* g) {
 void group_destroy(rr_group* g) {
     DeviceGuard device_guard;
     if (!g) return;
+    trace("group_destroy %p: %d parts, %lld frames; drain", (void*)g, g->nlocal(), (long long)g->k);
     group_drain(g);
+    trace("group_destroy %p: drained", (void*)g);
     for (ncclComm_t c : g->comms)
         if (c) (void)ncclCommDestroy(c);
+    // the parts' render contexts first: their last stream is the group's render stream of their set
+    // (rr_ctx::last_st), which rr_destroy synchronises and which must therefore still exist
+    for (int b = 0; b < 2; ++b)
+        for (size_t l = 0; l < g->subs[b].size(); ++l)
+            if (g->subs[b][l]) {
+                trace("group_destroy %p: context of part %zu set %d", (void*)g, l, b);
+                rr_destroy(g->subs[b][l]);
+                g->subs[b][l] = nullptr;
+            }
+    trace("group_destroy %p: contexts destroyed", (void*)g);
     for (size_t l = 0; l < g->devices.size(); ++l) {
         (void)hipSetDevice(g->devices[l]);
         for (int b = 0; b < 2; ++b) {
@@ -287,9 +304,7 @@ void group_destroy(rr_group* g) {
             if (g->ev_caller) (void)hipEventDestroy(g->ev_caller);
         }
     }
-    for (int b = 0; b < 2; ++b)
-        for (rr_ctx* s : g->subs[b])
-            if (s) rr_destroy(s);
+    trace("group_destroy %p: done", (void*)g);
     delete g;
 }
 
@@ -421,8 +436,12 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
         GHIP(hipEventRecord(g->ev_caller, caller));
     }
     bool enqueued = false;
+    trace("group_render_gather %p: frame %lld, %d parts, %lld x %lld, block %d", (void*)g, (long long)g->k, n,
+          (long long)W, (long long)H, block);
     const int rc = enqueue_frame(g, cam, opts, static_cast<double*>(d_frame), caller, W, H, block, b, enqueued);
     if (rc != RR_OK) {
+        trace("group_render_gather %p: error %d after %s: %s", (void*)g, rc, enqueued ? "enqueuing" : "no work",
+              rr_last_error());
         if (enqueued) {  // drain what this call enqueued before reporting: nothing of a failed frame stays in flight
             const std::string msg = rr_last_error();
             group_drain(g);
@@ -430,6 +449,7 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
         }
         return rc;
     }
+    trace("group_render_gather %p: frame %lld enqueued", (void*)g, (long long)g->k);
     ++g->k;
     return RR_OK;
 }
@@ -451,6 +471,7 @@ int group_render(rr_group* g, const rr_camera* cam, const rr_render_opts* o, dou
     so.flags = RR_OUT_AVG;
     int rc = group_render_gather(g, cam, &so, g->root_here() ? g->frame.p : nullptr, nullptr);
     if (rc != RR_OK) return rc;
+    trace("group_render %p: synchronise", (void*)g);
     for (int l = 0; l < g->nlocal(); ++l) {  // every stream synchronised: a failure here leaves nothing in flight either
         GHIP(hipSetDevice(g->devices[l]));
         for (int b = 0; b < 2; ++b) {
@@ -470,6 +491,7 @@ int group_render(rr_group* g, const rr_camera* cam, const rr_render_opts* o, dou
         GHIP(hipSetDevice(g->devices[0]));
         GHIP(hipMemcpy(out_avg, g->frame.p, (size_t)W * H * 3 * sizeof(double), hipMemcpyDeviceToHost));
     }
+    trace("group_render %p: synchronised", (void*)g);
     rr_stats local;
     rc = group_last_stats(g, stats ? stats : &local);
     if (rc != RR_OK) return rc;

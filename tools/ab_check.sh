@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/check
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread \
+  RRAY_TRACE_FILE=$PWD/gpurun_out/check/trace.log timeout -k 10 600 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread \
     > gpurun_out/check/gpu_tests.log 2>&1 || { tail -30 gpurun_out/check/gpu_tests.log; exit 1; }
   tail -1 gpurun_out/check/gpu_tests.log
 fi
