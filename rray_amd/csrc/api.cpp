@@ -99,7 +99,12 @@ struct rr_ctx {
     unsigned long long* stats_src = nullptr;  // buffer holding the last frame's counters
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipEvent_t ev_in = nullptr, ev_out = nullptr;
-    hipStream_t last_st = nullptr;  // stream of the last render (the context's workspace is ordered on it)
+    // the stream of the last render (compared, never used: a caller may destroy its stream before the context) and
+    // ev_out, recorded after the last render's work on it — what later renders on other streams and the context's
+    // teardown wait for (the round-4 teardown hang: rr_destroy synchronised a group's render stream after the group
+    // had destroyed it)
+    hipStream_t last_st = nullptr;
+    bool have_out = false;
     // canvas-path frames: the per-pass box averages run on aa_stream (run_levels AaPasses)
     hipStream_t aa_stream = nullptr;
     std::vector<hipEvent_t> pass_ev;
@@ -163,17 +168,22 @@ rr::DevCamera dev_camera(const rr_camera* c) {
 // The context's workspace is used on one stream at a time: a call on another stream than the
 // previous one first waits for it (one event, only when the stream changes).
 hipError_t claim_stream(rr_ctx* c, hipStream_t st) {
-    if (c->last_st && c->last_st != st) {
-        hipError_t e = hipEventRecord(c->ev_in, c->last_st);
-        if (e == hipSuccess) e = hipStreamWaitEvent(st, c->ev_in, 0);
+    if (c->have_out && c->last_st != st) {
+        hipError_t e = hipStreamWaitEvent(st, c->ev_out, 0);
         if (e != hipSuccess) return e;
     }
     c->last_st = st;
     return hipSuccess;
 }
+// marks the end of the work a call enqueued on `st` (claim_stream and sync_ctx wait for it)
+hipError_t release_stream(rr_ctx* c, hipStream_t st) {
+    hipError_t e = hipEventRecord(c->ev_out, st);
+    if (e == hipSuccess) c->have_out = true;
+    return e;
+}
 hipError_t sync_ctx(rr_ctx* c) {
     hipError_t e = hipStreamSynchronize(c->stream);
-    if (e == hipSuccess && c->last_st && c->last_st != c->stream) e = hipStreamSynchronize(c->last_st);
+    if (e == hipSuccess && c->have_out) e = hipEventSynchronize(c->ev_out);
     return e;
 }
 
@@ -1000,6 +1010,7 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     c->stats_src = frame_counters(c, c->epoch);
     c->epoch ^= 1;
     if (c->frame_timed) HIPCHK(hipEventRecord(c->e1, st));
+    HIPCHK(release_stream(c, st));
     c->stats_pending = true;
     // C_SAMPLES is not incremented by the wavefront kernels; it is the level-0 event count
     c->last.samples = (uint64_t)total;
@@ -1126,6 +1137,7 @@ int rr_color_at(rr_ctx* c, int64_t n, const double* origins, const double* direc
     // the counters on the same (non-blocking) stream, then wait: out_rgb and the counters are both
     // complete on return, whatever kind of host memory the caller passed
     HIPCHK(hipMemcpyAsync(c->h_counters, frame_counters(c, 2), kCounterBytes, hipMemcpyDeviceToHost, st));
+    HIPCHK(release_stream(c, st));
     HIPCHK(hipStreamSynchronize(st));
     rr_stats q;
     collect_stats(c, &q);
@@ -1149,6 +1161,7 @@ int rr_is_shadowed(rr_ctx* c, int64_t n, const double* points, const double* lig
     HIPCHK(rr::launch_shadow_query(c->S, c->rays0.as<double>(), c->rays0.as<double>() + 3 * n, n,
                                    c->qout.as<int32_t>(), frame_counters(c, 2), st));
     HIPCHK(hipMemcpyAsync(out, c->qout.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(release_stream(c, st));
     HIPCHK(hipStreamSynchronize(st));
     return RR_OK;
 }

@@ -263,3 +263,37 @@ def test_failed_group_frame_drains_its_work(R, single, monkeypatch):
         assert np.array_equal(g.render(scene.camera, aa=aa)["avg"], ref["avg"])
     finally:
         g.close()
+
+
+def test_context_outlives_the_caller_stream(R):
+    """A context renders on a caller's stream that the caller destroys afterwards; the context then renders on a
+    second stream and is destroyed.  Neither step touches the destroyed stream (the context waits on an event of its
+    own, rr_ctx::ev_out): the round-4 teardown hang came from synchronising a group's destroyed render stream in
+    rr_destroy.  Both frames equal the context's own-stream render bit for bit."""
+    import time
+
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    scene = _scene(R, "c3_s1024_reflect.yaml", 48, 40, 3)
+    r = R.Renderer(0)
+    d = ctypes.c_void_p()
+    try:
+        r.upload(scene)
+        ref = r.render(scene.camera, aa=3)["avg"]
+        nbytes = ref.size * 8
+        assert hip.hipMalloc(ctypes.byref(d), ctypes.c_size_t(nbytes)) == 0
+        opts = R._lib.RenderOpts(3, 5, 0, 0, 0, 1, 8, R._lib.RR_OUT_AVG | R._lib.RR_NO_FRAME_TIMING)
+        for _ in range(2):  # stream 1, destroyed; then stream 2, destroyed before the context
+            st = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(st)) == 0
+            r.render_device(scene.camera, opts, None, d.value, st.value)
+            assert hip.hipStreamSynchronize(st) == 0
+            out = np.empty_like(ref)
+            assert hip.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), d, ctypes.c_size_t(nbytes), 2) == 0
+            assert np.array_equal(out, ref)
+            assert hip.hipStreamDestroy(st) == 0
+    finally:
+        t0 = time.perf_counter()
+        r.close()
+        assert time.perf_counter() - t0 < 10.0
+        if d.value:
+            hip.hipFree(d)
