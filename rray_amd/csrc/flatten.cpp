@@ -244,6 +244,59 @@ void reorder_spatial(HostScene& hs) {
 
 // Runs of up to 64 consecutive nodes with a bounding sphere of their culls; unbounded nodes
 // (planes, unbounded groups) get a chunk of their own.
+// NF_OWN_SAFE (device_core.inc own_node): spheres and planes outside any CSG whose world-to-object transform A
+// (ancestors' inverses and the node's, as the walks apply them; linear part A_l, translation A_t) keeps every rounding
+// the skip's argument meets far inside its margin (factor 1e3).  The margin: an over point lies EPS = 1e-5 beyond the
+// tangent plane at the hit point, at least EPS sigma_min(A_l) in object space, sigma_min(A_l) >= 1 / |F_l|_F (F the
+// forward transform).  The roundings against it:
+//   * the object-space shadow origin, direction and quadratic: a few ulps of |A_l| |over| + |A_t|, for |over|_inf <= W
+//     = 1e5 (own_node checks W at run time); |A_l| <= 1e8 keeps a wrong-side direction component below the plane test's
+//     EPS;
+//   * the hit point itself: sphere.rs's roots come from b^2 - 4ac, which cancels when the incoming ray's object-space
+//     origin q0 is far from the unit sphere, and put the point up to ~4 eps |q0|^2 off the surface along the normal
+//     (a camera 2e4 units from a 3e-3 sphere: 2e-3 object units, inside the margin — fuzz seed 2).  |q0|_2 <=
+//     sqrt(3) (1.01 + |A_l|_inf T) with T = t |d|_inf of the hit, so the node stores the largest allowed T (float bits
+//     in DevNode.aux, unused by spheres and planes) and prepare() compares the hit's T with it.
+// Infinity norms throughout.
+static void mark_own_safe(HostScene& hs) {
+    const double eps = 0x1p-52, W = 1e5, EPS = 1e-5, SAFETY = 1e3;
+    for (size_t ni = 0; ni < hs.nodes.size(); ++ni) {
+        DevNode& nd = hs.nodes[ni];
+        if ((nd.kind != RR_SPHERE && nd.kind != RR_PLANE) || (nd.flags & NF_IN_CSG)) continue;
+        M4 fwd = identity(), inv = identity();
+        for (int a = (int)ni; a >= 0; a = hs.nodes[a].parent) {
+            M4 nfull = identity();
+            for (int e = 0; e < 12; ++e) nfull.m[e] = hs.nodes[a].inv[e];
+            inv = multiply(inv, nfull);  // the node's inverse first, the root's last: A = inv_node ... inv_root
+            fwd = multiply(inverse(nfull), fwd);
+        }
+        double al = 0.0, at = 0.0, ff = 0.0;
+        bool finite = true;
+        for (int r = 0; r < 3; ++r) {
+            double row = 0.0;
+            for (int c = 0; c < 3; ++c) {
+                row += std::fabs(inv.m[4 * r + c]);
+                ff += fwd.m[4 * r + c] * fwd.m[4 * r + c];
+            }
+            al = std::fmax(al, row);
+            at = std::fmax(at, std::fabs(inv.m[4 * r + 3]));
+            for (int c = 0; c < 4; ++c) finite = finite && std::isfinite(inv.m[4 * r + c]) && std::isfinite(fwd.m[4 * r + c]);
+        }
+        const double fn = std::sqrt(ff);
+        if (!finite || !(fn > 0.0) || !(al <= 1e8) || !(al > 0.0)) continue;
+        const double sigma_min = 1.0 / fn, margin = EPS * sigma_min;
+        if (!(SAFETY * 4.0 * eps * (al * (2.0 * W + 1.0) + at) <= margin)) continue;
+        // 4 eps * 3 (1.01 + al T)^2 * SAFETY <= margin
+        const double tlim = (std::sqrt(margin / (12.0 * eps * SAFETY)) - 1.01) / al;
+        if (!(tlim > 0.0)) continue;
+        const float tl = (float)(tlim * (1.0 - 1e-6));
+        int32_t bits;
+        std::memcpy(&bits, &tl, sizeof bits);
+        nd.aux = bits;
+        nd.flags |= NF_OWN_SAFE;
+    }
+}
+
 void build_chunks(HostScene& hs) {
     hs.chunks.clear();
     const int N = (int)hs.nodes.size();
@@ -755,6 +808,7 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
         ++n_inline;
     }
     out.tri_inline = n_tri > 0 && n_inline == n_tri ? 1 : 0;
+    mark_own_safe(out);
     for (DevChunk& ch : out.chunks) {  // runs of one kind (DevChunk.run)
         ch.run = CR_NONE;
         const DevNode& a = out.nodes[ch.start];

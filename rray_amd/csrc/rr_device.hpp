@@ -20,6 +20,9 @@ enum NodeFlags : int32_t {
     NF_TRI_INLINE = 8,  // triangle with an identity inverse (every OBJ face): inv[0..8] hold its p1, e1, e2
                         // (DevTri order), so the walk's exact test needs no dependent DevTri load; the
                         // identity itself is implied by NF_IDENT (also set)
+    NF_OWN_SAFE = 16,   // sphere / plane outside any CSG whose world-to-object transform is conditioned well enough
+                        // that a shadow ray leaving its own surface point outward cannot hit it (flatten.cpp
+                        // mark_own_safe; the walks skip that exact test, device_core.inc walk_nodes `own`)
     NF_CSG_LHIT0 = 256, // bit (8 + d): for the CSG at position d of this leaf's ancestor chain,
                         // left.includes(this leaf) (csg.rs:86-88 with Object::includes semantics)
 };
