@@ -95,7 +95,7 @@ struct CombArgs {
 // stage (scenes with an area light).
 constexpr int RR_PRELIT_LIGHTS = 2;
 constexpr size_t RR_AREA_STAGE_BYTES = 3 * 256 * 8 + 3 * 256 * 4;
-constexpr size_t RR_CHAIN_STAGE_BYTES = 10 * 256 * 8 + 3 * 256 * 4;  // chain kernels: parked ray, level-0 record, Px0
+constexpr size_t RR_CHAIN_STAGE_BYTES = 10 * 256 * 8 + 4 * 256 * 4;  // chain kernels: parked ray, level-0 record, Px0, own
 
 // Level-0 camera events run in 8x8-sample tiles of the part-local supersampled canvas (8-row bands,
 // 8-column tiles inside a band; the last band / column may be narrower) so that a wave's 64 rays

@@ -83,7 +83,8 @@ def beyond_tangent(corners, over, n):
 
 
 def check_scene(o, kinds, lights, rays, depth=1, areas=(), rng=None):
-    """Shadow rays of the hits of `rays` (and of their reflections, `depth` bounces): (skips, violations).  areas:
+    """Shadow rays and reflected rays of the hits of `rays` (and of their reflections, `depth` bounces): (skips,
+    violations); a reflected ray must find no entry t >= 0 on the object it leaves (reflect_own).  areas:
     (corner, u, v) of area lights, whose rays toward 16 random points of the light and its corners are checked where
     area_beyond_tangent allows the skip."""
     rng = rng or np.random.default_rng(0)
@@ -112,6 +113,12 @@ def check_scene(o, kinds, lights, rays, depth=1, areas=(), rng=None):
         T = xs[h][0] * np.abs(np.array(d[:3])).max()
         if lim is None or not T <= lim or not np.abs(over).max() <= W_OVER:
             continue
+        rv = np.array(c["reflectv"][:3])
+        if rv[0] * n[0] + rv[1] * n[1] + rv[2] * n[2] >= 1e-6:  # reflect_own: the reflected ray's closest-hit walk
+            skips += 1
+            sx = o.intersect(tuple(over) + (1.0,), tuple(rv) + (0.0,))
+            if any(ob == obj and t >= 0.0 for (t, ob, _, _) in sx):
+                viol += 1
         for L in lights:
             v = np.array(L) - over
             dist = math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2])
