@@ -52,7 +52,7 @@ def scene_dir(scene_file):
     return os.path.dirname(os.path.normpath(os.path.join(ROOT, "scenes", scene_file)))
 SINGLE_GPU_WORKLOAD = "c2_s1024"      # BASELINE configs[1]
 MULTI_GPU_WORKLOAD = "c3_s1024_reflect"  # BASELINE configs[2]
-BLOCK = 8  # output rows per interleaved block
+BLOCK = int(os.environ.get("RRAY_BLOCK_ROWS", "8"))  # output rows per interleaved block (env: experiments)
 DEPTH_OVERRIDE = None  # --max-depth (experiments only)
 # SURVEY.md §8(d) algorithmic flop model (FMA = 2, sqrt/div = 1): per leaf test and per shade event
 FLOPS = {"sphere": 57, "plane": 13, "tri": 45, "group": 45, "shade": 250}
