@@ -342,6 +342,82 @@ def build_area(seed):
     return P, {"from_": frm, "to": to, "up": (0.0, 1.0, 0.0), "fov": fov}, 3, f"area{kind}"
 
 
+def build_own(seed):
+    """Scenes for the own-object skip (shadow and reflected rays skip the object they leave): lights on
+    or next to the tangent planes of the spheres the camera sees (light . normal ~ 0), lights inside spheres, the camera
+    inside a sphere (inside hits: no skip), anisotropic and sheared spheres, tilted and scaled planes, spheres from 1e-3
+    to 1e3 units, far cameras with narrow fields of view (the hit-distance limit of flatten.cpp mark_own_safe), mirrors
+    viewed at grazing angles, an area light straddling a sphere's tangent planes.  -> (Pair, camera spec, depth,
+    category)."""
+    rng = np.random.default_rng(30_000 + seed)
+    P = Pair()
+    M = P.M
+    kind = seed % 6
+    cat = ["tangent_light", "light_inside", "camera_inside", "aniso_planes", "far_small", "area_straddle"][kind]
+    depth = 4
+    frm, to, fov = (0.0, 2.0, -8.0), (0.0, 0.5, 0.0), 1.0
+    centres = []
+    for _ in range(int(rng.integers(3, 9))):
+        r = _logu(rng, 0.2, 1.5)
+        c = np.array([rng.uniform(-3, 3), r * rng.uniform(0.5, 1.5), rng.uniform(-2, 3)])
+        if kind == 3 and rng.random() < 0.6:
+            tr = _mul(M, M.scale(r * rng.uniform(0.2, 3.0), r, r * rng.uniform(0.2, 3.0)), _rot(M, rng),
+                      M.shear(*[float(x) for x in rng.uniform(-0.5, 0.5, 6)]), M.translate(*[float(x) for x in c]))
+        else:
+            tr = _mul(M, M.scale(r, r, r), M.translate(*[float(x) for x in c]))
+        P.obj("sphere", tr, _material(rng, reflective_p=0.6), _color(rng))
+        centres.append((c, r))
+    tilt = float(rng.uniform(-0.2, 0.2)) if kind == 3 else 0.0
+    sc = float(rng.choice([1.0, 1e-3, 50.0])) if kind == 3 else 1.0
+    P.obj("plane", _mul(M, M.scale(sc, sc, sc), M.rotate("z", tilt)), _material(rng, reflective_p=0.6), _color(rng))
+    c, r = centres[0]
+    if kind == 0:  # lights on the tangent planes of points the camera sees: light . normal ~ 0 at those points
+        for _ in range(2):
+            n = _unit(rng)
+            n[2] = -abs(n[2])  # facing the camera
+            n /= np.linalg.norm(n)
+            t = np.cross(n, _unit(rng))
+            t /= np.linalg.norm(t)
+            P.light(c + r * n + t * rng.uniform(2, 10) + n * float(rng.choice([0.0, 1e-9, -1e-9, 1e-6])))
+    elif kind == 1:  # a light inside a sphere, another just above a surface
+        P.light(c + _unit(rng) * r * 0.5)
+        n = _unit(rng)
+        P.light(c + n * r * (1.0 + 1e-7))
+    elif kind == 2:  # the camera inside a big sphere (glass-free: inside hits shade the inner wall)
+        P.obj("sphere", _mul(M, M.scale(30.0, 30.0, 30.0)), _material(rng, reflective_p=0.6), _color(rng))
+        P.light(rng.uniform(-5, 5, 3) + [0, 8, 0])
+    elif kind == 3:
+        P.light(rng.uniform(-10, 10, 3) + [0, 12, -6])
+    elif kind == 4:  # spheres from 1e-3 to 1e3 units, seen from 10^2..10^4.5 units away with a narrow field of view
+        s = _logu(rng, 1e-3, 1e3)
+        for _ in range(4):
+            P.obj("sphere", _mul(M, M.scale(s, s, s), M.translate(*[float(x) for x in rng.uniform(-3, 3, 3) * s])),
+                  _material(rng, reflective_p=0.6), _color(rng))
+        P.light(rng.uniform(-10, 10, 3) * s + [0, 12 * s, 0])
+        dist = _logu(rng, 1e2, 3e4) * max(s, 1.0)
+        frm = tuple(float(x) for x in _unit(rng) * dist)
+        to = (0.0, 0.0, 0.0)
+        fov = float(8.0 * s / dist)
+    else:  # an area light whose parallelogram straddles the tangent planes of the first sphere's visible points
+        n = np.array([0.0, 0.3, -1.0])
+        n /= np.linalg.norm(n)
+        q = c + r * n
+        u = np.cross(n, [0.0, 1.0, 0.0])
+        u /= np.linalg.norm(u)
+        P.area_light(q + n * float(rng.uniform(-0.5, 0.5)) - u * 2.0 + np.array([0.0, 1.5, 0.0]), u * 4.0,
+                     np.array([0.0, 1.0, 0.0]) * float(rng.uniform(0.5, 2.0)), int(rng.integers(2, 5)))
+        depth = 3
+    if kind in (0, 1, 3) and rng.random() < 0.5:  # grazing view of a mirror: the camera near a sphere's silhouette
+        frm = tuple(float(x) for x in c + np.array([r * 1.02, 0.0, -6.0]))
+        to = tuple(float(x) for x in c + np.array([r, 0.0, 0.0]))
+        fov = 0.3
+    if kind == 2:
+        frm, to, fov = (0.0, 1.0, -5.0), (0.0, 0.5, 2.0), 1.2
+    P.log.append(f"camera from={frm} to={to} fov={fov} depth={depth}")
+    return P, {"from_": tuple(float(x) for x in frm), "to": tuple(float(x) for x in to), "up": (0.0, 1.0, 0.0),
+               "fov": float(fov)}, depth, cat
+
+
 def cameras(P, spec, W, H):
     """Product and oracle cameras from the same view_transform (the oracle's matrix.rs restatement)."""
     import oracle

@@ -90,3 +90,32 @@ def test_area_light_fuzz_bit_exact(renderer, seed):
             print(f"  sample ({x},{y}): gpu {got['canvas'][y, x].tolist()} oracle {canvas_cr[y, x].tolist()}")
         print("\n".join(P.log))
     assert ok, f"seed {seed} ({cat})"
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_own_skip_fuzz_bit_exact(renderer, seed):
+    """The own-object skip (shadow and reflected rays skip the object they leave) at its edges
+    (tests/scene_fuzz.py build_own): lights on the tangent planes of visible points, lights inside spheres, the camera
+    inside a sphere, sheared spheres and scaled planes, 1e-3..1e3 spheres seen from far with narrow fields of view,
+    grazing mirrors, an area light straddling tangent planes.  The canvas must equal the oracle's (correctly rounded
+    powers) bit for bit, with the same ray counts."""
+    P, spec, depth, cat = F.build_own(seed)
+    aa = 2 if seed % 4 == 3 else 1
+    W, H = (24, 16) if aa == 2 else (40, 24)
+    cam, ocam = F.cameras(P, spec, W * aa, H * aa)
+    renderer.upload(P.b)
+    got = renderer.render(cam, aa=aa, max_depth=depth, seed=seed, canvas=True)
+    P.o.set_pow_mode(1)
+    canvas_cr, st = P.o.render(ocam, max_depth=depth, seed=seed)
+    P.o.set_pow_mode(0)
+    diff = np.argwhere((got["canvas"] != canvas_cr).any(axis=2))
+    counts = {k: (got["stats"][k], v) for k, v in (("rays", st["rays"] - st["shadow_rays"]),
+                                                    ("shadow_rays", st["shadow_rays"]),
+                                                    ("shade_events", st["shade_events"]))}
+    ok = len(diff) == 0 and all(a == b for a, b in counts.values())
+    if not ok:
+        print(f"seed {seed} ({cat}) {W}x{H} aa{aa}: {len(diff)} samples differ; counts (gpu, oracle) {counts}")
+        for y, x in diff[:10]:
+            print(f"  sample ({x},{y}): gpu {got['canvas'][y, x].tolist()} oracle {canvas_cr[y, x].tolist()}")
+        print("\n".join(P.log))
+    assert ok, f"seed {seed} ({cat})"

@@ -166,6 +166,36 @@ def test_own_object_never_shadows_where_skipped(seed):
     assert viol == 0, f"seed {seed} ({cat}): the own object shadows {viol} of {skips} skipped shadow rays"
 
 
+def _fuzz_lights(P):
+    lights = [tuple(float(x) for x in m.groups()) for line in P.log
+              for m in [re.match(r"point light \(([^,]+), ([^,]+), ([^)]+)\)", line)] if m]
+    areas = [tuple(tuple(float(x) for x in g.split(",")) for g in m.groups()) for line in P.log
+             for m in [re.match(r"area light corner=\(([^)]+)\) u=\(([^)]+)\) v=\(([^)]+)\)", line)] if m]
+    return lights, areas
+
+
+_OWN_SKIPS = []
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_own_object_never_shadows_in_edge_scenes(seed):
+    """tests/scene_fuzz.py build_own: the skip's edge cases (lights on tangent planes and inside spheres, the camera
+    inside a sphere, sheared spheres, scaled planes, far small spheres, grazing mirrors, area lights straddling tangent
+    planes), primary hits and two bounces."""
+    P, spec, depth, cat = F.build_own(seed)
+    _, ocam = F.cameras(P, spec, 40, 24)
+    lights, areas = _fuzz_lights(P)
+    skips, viol = check_scene(P.o, kinds_from_log(P), lights, camera_rays(ocam, 40, 24), depth=2, areas=areas)
+    _OWN_SKIPS.append(skips)
+    assert viol == 0, f"seed {seed} ({cat}): the own object shadows or blocks {viol} of {skips} skipped rays"
+
+
+def test_own_edge_scenes_exercise_the_skip():
+    if len(_OWN_SKIPS) < 48:
+        pytest.skip("runs after the edge-scene tests (same process)")
+    assert sum(_OWN_SKIPS) > 10000 and sum(1 for k in _OWN_SKIPS if k) >= 36, _OWN_SKIPS
+
+
 @pytest.mark.parametrize("wl,depth", [("c2_s1024", 0), ("c3_s1024_reflect", 2)])
 def test_own_skip_applies_in_the_benchmark_scenes(wl, depth):
     """The benchmark scenes (every 37th pixel of 1920 x 1080; C3's reflections to two bounces): the skip applies to
