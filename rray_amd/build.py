@@ -27,13 +27,14 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "
 DEVICE = ["--offload-arch=" + ARCH, "-mllvm", "-disable-promote-alloca-to-lds"]
 LEVEL_UNITS = [f"render_levels_g{g}_{lc}.hip" for g in (2, 1, 0) for lc in ("lds", "gl")]  # slowest first
 CHAIN_UNITS = [f"render_chain_g{g}_{lc}.hip" for g in (2, 1, 0) for lc in ("lds", "gl")]
+TREE_UNITS = [f"render_tree_g{g}_{lc}.hip" for g in (2, 1, 0) for lc in ("lds", "gl")]
 # per-unit flags: the chain kernels' loop must not get loop-invariant constants hoisted into registers (they
 # spill instead of being rematerialised)
-UNIT_FLAGS = {u: ["-mllvm", "-disable-machine-licm"] for u in CHAIN_UNITS}
+UNIT_FLAGS = {u: ["-mllvm", "-disable-machine-licm"] for u in CHAIN_UNITS + TREE_UNITS}
 # the flat scenes' global-cull level kernels (C2's fused camera kernel): the scheduler's AMDGPU register-pressure
 # trackers measured C2 0.1176 -> 0.1166 ms; the same flag on every unit cost C3 and C4 1 % (profiles/r05/ab_trackers.txt)
 UNIT_FLAGS["render_levels_g0_gl.hip"] = ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"]
-SOURCES = LEVEL_UNITS + CHAIN_UNITS + ["render.hip", "api.cpp", "multi.cpp", "flatten.cpp", "frontend.cpp", "yaml.cpp", "png.cpp", "jpeg.cpp",
+SOURCES = LEVEL_UNITS + CHAIN_UNITS + TREE_UNITS + ["render.hip", "api.cpp", "multi.cpp", "flatten.cpp", "frontend.cpp", "yaml.cpp", "png.cpp", "jpeg.cpp",
                                          "imgfmt.cpp"]
 
 

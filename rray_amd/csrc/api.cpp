@@ -181,6 +181,20 @@ hipError_t release_stream(rr_ctx* c, hipStream_t st) {
     if (e == hipSuccess) c->have_out = true;
     return e;
 }
+// Scope guard of a call's work on `st`: ev_out is recorded on every exit after claim_stream, error returns
+// included, so work a failed call already launched is still covered by what the next call and rr_destroy wait for.
+struct StreamClaim {
+    rr_ctx* c;
+    hipStream_t st;
+    bool released = false;
+    hipError_t release() {
+        released = true;
+        return release_stream(c, st);
+    }
+    ~StreamClaim() {
+        if (!released) (void)release_stream(c, st);
+    }
+};
 hipError_t sync_ctx(rr_ctx* c) {
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess && c->have_out) e = hipEventSynchronize(c->ev_out);
@@ -289,9 +303,11 @@ int tile_bundles(rr_ctx* c, const rr::LevelArgs& base_args, hipStream_t st, cons
 // sample spawns a secondary ray (fused levels with no reflective / transparent material, or depth 0).
 bool wave_avg_ok(const rr_ctx* c, int32_t aa, int64_t hs, int64_t local_rows, int max_depth) {
     // (reflection chains run inside the level-0 wave, chain_levels: every sample is final in its wave too)
+    // (and the color_at trees of transparent scenes, tree_levels, likewise)
     return (aa == 2 || aa == 4 || aa == 8) && hs % 8 == 0 && local_rows % 8 == 0 && local_rows > 0 &&
-           rr::fused_levels(c->S) &&
-           (c->host.max_children == 0 || max_depth == 0 || rr::chain_levels(c->S, c->host.max_children, max_depth));
+           ((rr::fused_levels(c->S) &&
+             (c->host.max_children == 0 || max_depth == 0 || rr::chain_levels(c->S, c->host.max_children, max_depth))) ||
+            rr::tree_levels(c->S));
 }
 
 // The box average of a canvas-path frame (aa outside the in-wave cases, e.g. C3's aa = 3) overlapped with the
@@ -308,8 +324,10 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
                void* avg = nullptr, int32_t avg_f32 = 0, int32_t aa_wave = 0, const AaPasses* aap = nullptr) {
     const bool ext = c->host.has_transparent != 0;
     const bool fused = rr::fused_levels(c->S);
-    // reflection chains inside the level-0 waves (chain_kernel): one level, no recursion queues
-    const bool chain = rr::chain_levels(c->S, c->host.max_children, max_depth);
+    // reflection chains inside the level-0 waves (chain_kernel), or the color_at trees of transparent scenes
+    // (tree_kernel): one level, no recursion queues
+    const bool tree = rr::tree_levels(c->S);
+    const bool chain = tree || rr::chain_levels(c->S, c->host.max_children, max_depth);
     const int k = chain ? 0 : c->host.max_children;
     const int plan_depth = chain ? 0 : max_depth;
     // batch: at most c->batch camera samples, shrunk (power-of-two steps, tile-aligned) until the
@@ -347,7 +365,7 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
         c->comb_ext.resize(P.levels);
         c->pend.resize(P.levels);
     }
-    if (!fused) {  // hit records and n1/n2 lists: the unfused trace / n1n2 / shade kernels only
+    if (!fused && !tree) {  // hit records and n1/n2 lists: the unfused trace / n1n2 / shade kernels only
         HIPCHK(c->hit.ensure(P.max_cap * sizeof(rr::HitRec)));
         HIPCHK(c->n12.ensure(P.max_cap * 2 * sizeof(double)));
         HIPCHK(c->n1n2.ensure(P.max_cap * sizeof(int32_t)));
@@ -364,7 +382,7 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
     // can send the chains still reflecting at depth RR_DEEP_FROM to a packed, segmented queue for a second launch.
     // Opt-in (RRAY_DEEP=1): on C3 the deep launch took 1.85 ms for what the camera waves did in 1.54 — the deep
     // rays' walks are latency-bound whether their waves are full or not
-    const bool spill = chain && aa_wave == 0 && !base_args.pw && max_depth >= rr::RR_DEEP_FROM && std::getenv("RRAY_DEEP") &&
+    const bool spill = chain && !tree && aa_wave == 0 && !base_args.pw && max_depth >= rr::RR_DEEP_FROM && std::getenv("RRAY_DEEP") &&
                        std::atoi(std::getenv("RRAY_DEEP")) == 1;
     const int64_t deep_seg_cap = (int64_t)256 << rr::RR_DEEP_SHIFT;
     const int64_t deep_nseg = (((B + 255) / 256) + (1 << rr::RR_DEEP_SHIFT) - 1) >> rr::RR_DEEP_SHIFT;
@@ -380,7 +398,7 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
     set_level0_index(T0);
     // chain frames order their camera waves too (tiles or pixel waves; the chains' depths spread tile costs widely)
     const int64_t n_tiles = T0.pw ? pixel_waves(T0) : T0.tile_fast ? T0.hs * T0.lrows / 64 : 0;
-    const bool order_ok = fused && !c->S.general && B >= total && n_tiles > 0 && n_tiles < ((int64_t)1 << 31) &&
+    const bool order_ok = (fused || tree) && !c->S.general && B >= total && n_tiles > 0 && n_tiles < ((int64_t)1 << 31) &&
                           n_tiles % 4 == 0 &&  // whole launch blocks (the group order permutes a block's four tiles)
                           (T0.pw || n_tiles * 64 == total) &&
                           ((c->S.has_groups && (k == 0 || max_depth == 0)) || (chain && !std::getenv("RRAY_NO_CHAIN_ORDER")));
@@ -480,7 +498,9 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
             }
             A.counters = frame_counters(c, c->epoch);
             A.counters_zero = (c->zero_next && d == 0 && base == 0) ? frame_counters(c, c->epoch ^ 1) : nullptr;
-            if (chain) {
+            if (tree) {
+                HIPCHK(rr::launch_tree(c->S, A, st, c->profile ? &c->prof : nullptr));
+            } else if (chain) {
                 if (spill) {  // camera launch appends to the deep queue's segments (level 1's counters)
                     A.deep = c->deep.as<rr::DeepRec>();
                     A.deep_from = rr::RR_DEEP_FROM;
@@ -966,11 +986,13 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     // a render on a different stream than the previous one first waits for that one.
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
     HIPCHK(claim_stream(c, st));
+    StreamClaim claim{c, st};
     // aa == 1, or aa in {2, 4, 8} without secondary rays (wave_avg_ok): the average is written by the
     // kernels directly; the canvas only when asked for
     const bool wave_avg = d_avg && wave_avg_ok(c, o->aa, cam->hsize, local_rows, o->max_depth);
     // aa == 3 frames with reflection chains: pixel waves (7 whole pixels per wave) average in the wave too
-    const bool pw = d_avg && !wave_avg && o->aa == 3 && rr::chain_levels(c->S, c->host.max_children, o->max_depth) &&
+    const bool pw = d_avg && !wave_avg && o->aa == 3 &&
+                    (rr::tree_levels(c->S) || rr::chain_levels(c->S, c->host.max_children, o->max_depth)) &&
                     block % 2 == 0 && total <= c->batch && !std::getenv("RRAY_NO_PW");
     const bool direct_avg = d_avg && (o->aa == 1 || wave_avg || pw);
     double* canvas = static_cast<double*>(d_canvas);
@@ -1010,7 +1032,7 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     c->stats_src = frame_counters(c, c->epoch);
     c->epoch ^= 1;
     if (c->frame_timed) HIPCHK(hipEventRecord(c->e1, st));
-    HIPCHK(release_stream(c, st));
+    HIPCHK(claim.release());
     c->stats_pending = true;
     // C_SAMPLES is not incremented by the wavefront kernels; it is the level-0 event count
     c->last.samples = (uint64_t)total;
@@ -1110,6 +1132,7 @@ int rr_color_at(rr_ctx* c, int64_t n, const double* origins, const double* direc
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
     HIPCHK(claim_stream(c, st));
+    StreamClaim claim{c, st};
     std::vector<double> rays((size_t)n * 6);
     for (int64_t i = 0; i < n; ++i)
         for (int k = 0; k < 3; ++k) {
@@ -1137,7 +1160,7 @@ int rr_color_at(rr_ctx* c, int64_t n, const double* origins, const double* direc
     // the counters on the same (non-blocking) stream, then wait: out_rgb and the counters are both
     // complete on return, whatever kind of host memory the caller passed
     HIPCHK(hipMemcpyAsync(c->h_counters, frame_counters(c, 2), kCounterBytes, hipMemcpyDeviceToHost, st));
-    HIPCHK(release_stream(c, st));
+    HIPCHK(claim.release());
     HIPCHK(hipStreamSynchronize(st));
     rr_stats q;
     collect_stats(c, &q);
@@ -1153,6 +1176,7 @@ int rr_is_shadowed(rr_ctx* c, int64_t n, const double* points, const double* lig
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
     HIPCHK(claim_stream(c, st));
+    StreamClaim claim{c, st};
     std::vector<double> buf((size_t)n * 6);
     std::memcpy(buf.data(), points, n * 3 * sizeof(double));
     std::memcpy(buf.data() + 3 * n, light_positions, n * 3 * sizeof(double));
@@ -1161,7 +1185,7 @@ int rr_is_shadowed(rr_ctx* c, int64_t n, const double* points, const double* lig
     HIPCHK(rr::launch_shadow_query(c->S, c->rays0.as<double>(), c->rays0.as<double>() + 3 * n, n,
                                    c->qout.as<int32_t>(), frame_counters(c, 2), st));
     HIPCHK(hipMemcpyAsync(out, c->qout.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    HIPCHK(release_stream(c, st));
+    HIPCHK(claim.release());
     HIPCHK(hipStreamSynchronize(st));
     return RR_OK;
 }

@@ -312,6 +312,8 @@ int decode_gif_rgba(const uint8_t* d, size_t n, std::vector<uint8_t>& rgba, uint
     const uint32_t fx = le16(d + pos), fy = le16(d + pos + 2), fw = le16(d + pos + 4), fh = le16(d + pos + 6);
     const uint32_t iflags = d[pos + 8];
     pos += 9;
+    // the frame's own size bounds the LZW output buffer: checked before anything is allocated for it
+    if (fw == 0 || fh == 0 || (uint64_t)fw * fh > kMaxTexels) return fail(err, RR_E_LIMIT, "GIF frame size");
     std::vector<uint8_t> lct;
     if (iflags & 0x80u) {
         const size_t sz = 3u << ((iflags & 7u) + 1);

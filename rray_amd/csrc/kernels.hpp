@@ -170,6 +170,13 @@ void launch_chain_t(const DevScene& S, const LevelArgs& A, hipStream_t stream, K
 // deep: the deep queue's launch (one block per segment, A.nseg segments), else the camera launch
 hipError_t launch_chain(const DevScene& S, const LevelArgs& A, hipStream_t stream, KernelProf* prof = nullptr,
                         bool deep = false);
+// Scenes with a transparent material: every camera sample's whole color_at tree (reflected and refracted children,
+// shade_hit's sums) inside its camera lane with an explicit per-lane stack (render_tree.inc tree_kernel), one launch
+// per batch with no recursion queues and no combine passes.  RRAY_NO_TREE=1 keeps the per-level kernels.
+bool tree_levels(const DevScene& S);
+template <int G, bool LC>
+void launch_tree_t(const DevScene& S, const LevelArgs& A, hipStream_t stream, KernelProf* prof);
+hipError_t launch_tree(const DevScene& S, const LevelArgs& A, hipStream_t stream, KernelProf* prof = nullptr);
 hipError_t launch_aa(const double* canvas, double* out, int64_t width, int64_t rows, int32_t aa, hipStream_t stream,
                      KernelProf* prof = nullptr);
 hipError_t launch_aa_f32(const double* canvas, float* out, int64_t width, int64_t rows, int32_t aa, hipStream_t stream,

@@ -344,6 +344,30 @@ hipError_t launch_chain(const DevScene& S, const LevelArgs& A, hipStream_t st, K
     return hipGetLastError();
 }
 
+bool tree_levels(const DevScene& S) { return S.has_transparent && !std::getenv("RRAY_NO_TREE"); }
+
+hipError_t launch_tree(const DevScene& S, const LevelArgs& A, hipStream_t st, KernelProf* prof) {
+    if (A.n <= 0) return hipSuccess;
+    const int g = S.general ? 2 : S.has_groups ? 1 : 0;
+    if (g == 2) {
+        if (S.lds_culls)
+            launch_tree_t<2, true>(S, A, st, prof);
+        else
+            launch_tree_t<2, false>(S, A, st, prof);
+    } else if (g == 1) {
+        if (S.lds_culls)
+            launch_tree_t<1, true>(S, A, st, prof);
+        else
+            launch_tree_t<1, false>(S, A, st, prof);
+    } else {
+        if (S.lds_culls)
+            launch_tree_t<0, true>(S, A, st, prof);
+        else
+            launch_tree_t<0, false>(S, A, st, prof);
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_combine(const CombArgs& C, hipStream_t st, KernelProf* prof) {
     if (C.n <= 0) return hipSuccess;
     Span s(prof, K_COMBINE, st);

@@ -110,10 +110,16 @@ class FramePipeline:
 
     def submit(self, i):
         ops = _post_transfer(self.tiles[i], self.stage, self.height, self.block, self.dst, self.group)
-        self.pending[i] = _Pending(ops)
+        pend = _Pending(ops, per_stream=self.tiles[i].is_cuda)
         if self.rank == self.dst:  # the current stream waits for the receives, then places the runs
-            self.pending[i].wait()
+            pend.wait()
             torch.index_select(self.stage, 0, self.src, out=self.frame)
+            # the root's own tile reaches the stage by a copy on the current stream, which no transfer operation
+            # covers: an event after it lets the renderer of frame k + depth (acquire's `prev`) wait for that read
+            if self.tiles[i].is_cuda:
+                pend.event = torch.cuda.Event()
+                pend.event.record()
+        self.pending[i] = pend
         self.k += 1
 
     def drain(self):
@@ -123,12 +129,21 @@ class FramePipeline:
 
 
 class _Pending:
-    """The operations of one frame's transfer, waited on together."""
+    """The operations of one frame's transfer, waited on together, and (on the root of a GPU pipeline) the event
+    recorded after the local reads of the tile.  On GPU tensors wait() orders the *current* stream after them and may
+    be called on several streams (an NCCL wait is a per-stream wait), so the operations are kept; on CPU tensors (gloo)
+    a wait blocks the host until the operation is done and gloo must not wait for a send twice (a second waitSend
+    waits for a send that never comes), so they are dropped once waited."""
 
-    def __init__(self, ops):
+    def __init__(self, ops, per_stream=False):
         self.ops = ops
+        self.per_stream = per_stream
+        self.event = None
 
     def wait(self):
         for op in self.ops:
             op.wait()
-        self.ops = []
+        if not self.per_stream:
+            self.ops = []
+        if self.event is not None:
+            self.event.wait()

@@ -396,12 +396,25 @@ def test_corrupt_textures_under_asan(tmp_path):
             f = tmp_path / f"{sd.stem}_{k}{sd.suffix}"
             f.write_bytes(bytes(m))
             files.append(str(f))
+    # GIF frames larger than the texel limit or empty: refused from the image descriptor, before the LZW buffers
+    # are sized (a 30-byte file must not reach a multi-GB allocation)
+    gif = bytearray((tmp_path / "s.gif").read_bytes())
+    at = gif.index(b"\x2c\x00\x00\x00\x00")  # the image descriptor (frame at 0, 0)
+    bad = []
+    for fw, fh in ((65535, 65535), (0, 13), (11, 0)):
+        m = bytearray(gif)
+        m[at + 5:at + 9] = bytes([fw & 255, fw >> 8, fh & 255, fh >> 8])
+        f = tmp_path / f"frame_{fw}x{fh}.gif"
+        f.write_bytes(bytes(m))
+        bad.append(str(f))
+    files += bad
     r = subprocess.run([exe] + [str(s) for s in seeds] + files, capture_output=True, text=True,
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0"))
     assert r.returncode == 0, r.stderr[-3000:]
     rcs = [int(line.split()[0]) for line in r.stdout.splitlines()]
     assert len(rcs) == len(seeds) + len(files)
     assert rcs[: len(seeds)] == [0] * len(seeds)  # the intact files decode
+    assert all(rc != 0 for rc in rcs[-len(bad):])  # the oversized and empty GIF frames are refused
 
 
 def test_group_contexts_need_a_device(R):

@@ -297,3 +297,45 @@ def test_context_outlives_the_caller_stream(R):
         assert time.perf_counter() - t0 < 10.0
         if d.value:
             hip.hipFree(d)
+
+
+def test_frame_pipeline_root_copy_orders_the_renderer(R):
+    """rray_amd.dist.FramePipeline on the root: its own tile reaches the stage by a copy on the current stream, which
+    no transfer operation covers.  The current stream here lags the render stream by a long sleep before each
+    submit, so without the event acquire() returns for the copy, the render of frame k + 2 (filling tile k mod 2 on
+    the render stream) would overwrite the tile before frame k's copy read it.  Every assembled frame must hold its
+    own frame's values."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from rray_amd.dist import FramePipeline
+
+    own = not dist.is_initialized()
+    if own:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        H, W = 40, 16
+        pipe = FramePipeline(H, W, 3, torch.float64, torch.device("cuda:0"), block=8, depth=2)
+        render = torch.cuda.Stream()
+        outs = []
+        for k in range(6):
+            i, tile, prev = pipe.acquire()
+            with torch.cuda.stream(render):
+                if prev is not None:
+                    prev.wait()
+                tile.fill_(float(k))
+            torch.cuda.current_stream().wait_stream(render)
+            torch.cuda._sleep(20_000_000)  # the current stream lags: this frame's copy of the tile runs late
+            pipe.submit(i)
+            outs.append(pipe.frame.clone())
+        torch.cuda.synchronize()
+        for k, f in enumerate(outs):
+            assert torch.all(f == float(k)).item(), k
+    finally:
+        if own:
+            dist.destroy_process_group()
