@@ -52,6 +52,8 @@ def scene_dir(scene_file):
     return os.path.dirname(os.path.normpath(os.path.join(ROOT, "scenes", scene_file)))
 SINGLE_GPU_WORKLOAD = "c2_s1024"      # BASELINE configs[1]
 MULTI_GPU_WORKLOAD = "c3_s1024_reflect"  # BASELINE configs[2]
+# the library group's partition (--partition): cost-balanced row bands (ABI 10 default) or interleaved 8-row blocks
+PARTITION = "bands"
 BLOCK = int(os.environ.get("RRAY_BLOCK_ROWS", "8"))  # output rows per interleaved block (env: experiments)
 DEPTH_OVERRIDE = None  # --max-depth (experiments only)
 # SURVEY.md §8(d) algorithmic flop model (FMA = 2, sqrt/div = 1): per leaf test and per shade event
@@ -135,13 +137,18 @@ def main():
                     help="tiles at N>1: the library's own RCCL group (rr_create_rank + rr_render_gather_device; the "
                          "torch process group only carries host-side coordination over gloo) or torch.distributed's "
                          "per-part RCCL send / receive of the tiles (rray_amd/dist.py FramePipeline)")
+    ap.add_argument("--partition", choices=("bands", "interleave"), default="bands",
+                    help="tiles at N>1 with --gather abi: cost-balanced row bands received straight into the frame "
+                         "(the library default) or interleaved 8-row tiles through a staging buffer and placement "
+                         "kernels (RR_PART_INTERLEAVE)")
     ap.add_argument("--force-dist", action="store_true",
                     help="rehearsal: run the multi-rank path (RCCL process group, pipelined gather) even at 1 rank")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank path: gloo, oracle-rendered thumbnail tiles, no GPU")
     args = ap.parse_args()
-    global DEPTH_OVERRIDE
+    global DEPTH_OVERRIDE, PARTITION
     DEPTH_OVERRIDE = args.max_depth
+    PARTITION = args.partition
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args))
@@ -234,7 +241,8 @@ class Session:
             if rank == 0:
                 self.frame_t = torch.zeros((self.H, self.W, 3), dtype=torch.float64, device=dev)
             self.opts = R._lib.RenderOpts(self.aa, self.depth, 0, 0, 0, 1, BLOCK,
-                                          R._lib.RR_OUT_AVG | R._lib.RR_NO_FRAME_TIMING)
+                                          R._lib.RR_OUT_AVG | R._lib.RR_NO_FRAME_TIMING |
+                                          (R._lib.RR_PART_INTERLEAVE if PARTITION == "interleave" else 0))
             self.stream = torch.cuda.current_stream(dev)
         else:
             # f64 tiles (bit-identical to the 1-GPU image), double-buffered: rendering frame k+1 overlaps
@@ -583,7 +591,9 @@ def gpu_bench(args, world, mode, workload):
     if rank == 0:
         via = ("library RCCL group: rr_create_rank + rr_render_gather_device" if args.gather == "abi" else
                "torch.distributed RCCL isend / irecv per part")
-        par = (f"row-tiles x{world} + rccl send/recv per part (f64 tiles, pipelined; {via})" if world > 1 or sess.multi else
+        part_kind = ("cost-balanced row bands" if PARTITION == "bands" else "interleaved 8-row tiles") \
+            if args.gather == "abi" else "interleaved 8-row tiles"
+        par = (f"{part_kind} x{world} + rccl send/recv per part (f64 tiles, pipelined; {via})" if world > 1 or sess.multi else
                "single GPU, whole frame") if tiles else \
             f"frame-parallel x{world} (one whole frame per rank per step, no data-path collective)"
         line = {"metric": METRIC, "value": round(value, 3), "unit": "Mpixel-samples/s", "n_gpus": world,
@@ -600,6 +610,7 @@ def gpu_bench(args, world, mode, workload):
                 "frames_in_flight": 2 if sess.multi and args.gather == "abi" else len(sess.slots or [0]),
                 "serial": serial,
                 "tile_identity": identity, "scaling_anchor": anchor, "single_gpu": single,
+                "bands": sess.rend.bands() if sess.multi and args.gather == "abi" else None,
                 "speedup_vs_single_gpu": round(value / single["value"], 3) if single else None,
                 "kernels_ms_per_step": {k: round(v[0] / steps, 4) for k, v in ktimes.items() if v[1]},
                 "host_enqueue_ms_per_step": round(t_enq / steps * 1e3, 4),

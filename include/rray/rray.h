@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 9
+#define RR_ABI_VERSION 10
 
 /* error codes */
 #define RR_OK 0
@@ -135,6 +135,10 @@ typedef struct {
     int32_t part, nparts;  /* row sharding: output rows y with (y/block_rows)%nparts == part */
     int32_t block_rows;    /* rows per interleaved block (default 8) */
     int32_t flags;         /* RR_OUT_* */
+    /* ABI 10: a contiguous band of output rows [row_begin, row_end) instead of an interleaved part (part 0 of 1
+       only; row_begin == row_end == 0: no band, and any other pair with row_end <= row_begin is refused).  Rows, pixels and the area-light jitter are the full frame's, so a band equals
+       those rows of the whole frame bit for bit. */
+    int32_t row_begin, row_end;
 } rr_render_opts;
 #define RR_OUT_CANVAS 1    /* write the supersampled canvas (Canvas.pixels layout) */
 #define RR_OUT_AVG 2       /* write the AA-averaged image (canvas.rs:76-96, before `as u8`) */
@@ -142,6 +146,8 @@ typedef struct {
                               pixel; the average itself is computed in f64) — compact tiles for gathers */
 #define RR_NO_FRAME_TIMING 8 /* rr_render_device only: no HIP event pair around the frame (each event
                                 record costs the stream a few microseconds); rr_stats.kernel_ms is 0 */
+#define RR_PART_INTERLEAVE 16 /* ABI 10, multi-device contexts: interleaved row tiles, a staging buffer and placement
+                                 kernels on rank 0 (the ABI 9 transfer) instead of cost-balanced bands */
 
 typedef struct {
     uint64_t rays;          /* closest-hit rays (primary + reflected + refracted) */
@@ -175,11 +181,16 @@ void rr_destroy(rr_ctx* ctx);
 int rr_scene_upload(rr_ctx* ctx, const rr_scene_desc* desc);
 
 /* ---- multi-device contexts (ABI 5): one frame across several GPUs (camera.rs:107-121 spreads one
- * frame over every rayon worker).  Global rank r renders the output rows {y : (y/block_rows) % N == r}
- * as an f64 AA-averaged tile.  One RCCL group per frame (over xGMI): every rank sends its whole tile to
- * rank 0 in one ncclSend, and rank 0 receives every part's tile (its own from itself) back to back into a
- * staging buffer of `height` rows, one ncclRecv per part (part p at row rr_stage_row_offset); one copy
- * kernel per part then places the tile's rows into their frame rows on the transfer stream.  The context
+ * frame over every rayon worker).  ABI 10 default: global rank r renders a contiguous band of output rows
+ * [bounds[r], bounds[r+1]) as an f64 AA-averaged tile; the bands are balanced by cost on the first frame of a
+ * layout (rank 0 renders that frame once as 64 timed bands, rr_balance_bands, and broadcasts the bounds to every
+ * rank: one ncclBroadcast per layout), and rank 0's band is kept lighter by its own transfer work.  One RCCL group
+ * per frame (over xGMI): every other rank sends its tile to rank 0 in one ncclSend, which rank 0 receives straight
+ * into the frame's rows; rank 0 copies its own tile there.  No staging buffer, no placement kernel.
+ * With RR_PART_INTERLEAVE (the ABI 9 transfer): rank r renders the output rows {y : (y/block_rows) % N == r};
+ * every rank sends its whole tile to rank 0 in one ncclSend, and rank 0 receives every part's tile (its own from
+ * itself) back to back into a staging buffer of `height` rows, one ncclRecv per part (part p at row
+ * rr_stage_row_offset); one copy kernel per part then places the tile's rows into their frame rows.  The context
  * owns a render and a transfer stream per device and the RCCL communicator.  rr_render (blocking; out_avg filled on rank 0 only) and
  * rr_render_gather_device (asynchronous) take part 0 of 1: the context does the split.  Only the
  * f64 averaged image is produced (no RR_OUT_CANVAS / RR_OUT_AVG_F32).  rr_color_at / rr_is_shadowed /
@@ -199,6 +210,16 @@ int rr_context_info(const rr_ctx* ctx, int32_t* nranks, int32_t* rank, int32_t* 
  * staging buffer.  For exercising / testing the multi-GPU frame assembly on one GPU; images are
  * bit-identical to one part's. */
 int rr_create_virtual(int device, int nparts, rr_ctx** out);
+/* ABI 10: band bounds from per-row costs: bounds[0] = 0 <= bounds[1] <= ... <= bounds[nparts] = height, every inner
+ * bound a multiple of `align`, such that part p's cost sum(row_cost[bounds[p] .. bounds[p+1]-1]) (plus root_extra
+ * for part 0, the same unit) is as even as the alignment allows.  Host only.  Returns RR_OK. */
+int rr_balance_bands(const double* row_cost, int64_t height, int32_t nparts, double root_extra, int32_t align,
+                     int64_t* bounds);
+/* ABI 10: the band bounds of a multi-device context (nranks + 1 values; n >= nranks + 1) once its first band frame
+ * has calibrated them, and rr_group_set_bands to impose bounds (every rank the same; skips the calibration until the
+ * frame layout changes).  rr_group_bands returns the number of bounds written (0: not calibrated yet). */
+int rr_group_bands(rr_ctx* ctx, int64_t* bounds, int32_t n);
+int rr_group_set_bands(rr_ctx* ctx, const int64_t* bounds, int32_t n);
 /* ABI 9: first row of part `part`'s tile in the staging buffer (the rows of parts 0 .. part-1; partition.hpp
  * stage_row_offset).  part == nparts gives height. */
 int64_t rr_stage_row_offset(int64_t height, int32_t part, int32_t nparts, int32_t block_rows);

@@ -9,6 +9,7 @@ from ._lib import LIB_PATH, RRError, lib  # noqa: F401
 from .render import (  # noqa: F401
     Renderer,
     SceneBuilder,
+    balance_bands,
     YamlScene,
     camera,
     device_count,
@@ -23,5 +24,5 @@ from .render import (  # noqa: F401
 )
 
 __all__ = ["Renderer", "SceneBuilder", "YamlScene", "camera", "part_rows", "quantize", "write_png",
-           "render_scene_from_str", "render_scene_from_file", "device_count", "rccl_unique_id", "stage_row_offset", "unshuffle", "RRError",
+           "render_scene_from_str", "render_scene_from_file", "device_count", "rccl_unique_id", "stage_row_offset", "unshuffle", "balance_bands", "RRError",
            "lib"]

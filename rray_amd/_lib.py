@@ -23,6 +23,7 @@ ERRORS = {-1: "RR_E_ARG", -2: "RR_E_HIP", -3: "RR_E_SCENE", -4: "RR_E_NONAFFINE"
 globals().update({name: code for code, name in ERRORS.items()})  # RR_E_ARG = -1, ...
 RR_OUT_CANVAS, RR_OUT_AVG, RR_OUT_AVG_F32 = 1, 2, 4
 RR_NO_FRAME_TIMING = 8  # rr_render_device: no per-frame HIP event pair (rr_stats.kernel_ms = 0)
+RR_PART_INTERLEAVE = 16  # multi-device contexts: interleaved tiles + staging buffer + placement (ABI 9) instead of bands
 SPHERE, PLANE, GROUP, TRIANGLE, SMOOTH_TRIANGLE, CUBE, CYLINDER, CONE, CSG, TORUS = range(10)
 CSG_OPS = {"union": 0, "intersection": 1, "difference": 2}
 PAT = {"test": 0, "solid": 1, "stripe": 2, "gradient": 3, "ring": 4, "checker": 5, "blend": 6, "perturbed": 7,
@@ -53,7 +54,8 @@ class Camera(C.Structure):
 
 class RenderOpts(C.Structure):
     _fields_ = [("aa", C.c_int32), ("max_depth", C.c_int32), ("seed", C.c_uint64), ("jitter_mode", C.c_int32),
-                ("part", C.c_int32), ("nparts", C.c_int32), ("block_rows", C.c_int32), ("flags", C.c_int32)]
+                ("part", C.c_int32), ("nparts", C.c_int32), ("block_rows", C.c_int32), ("flags", C.c_int32),
+                ("row_begin", C.c_int32), ("row_end", C.c_int32)]
 
 
 class Stats(C.Structure):
@@ -76,7 +78,8 @@ EXPORTS = ["rr_abi_version", "rr_last_error", "rr_device_count", "rr_create", "r
            "rr_is_shadowed", "rr_scene_inspect", "rr_scene_from_yaml", "rr_scene_desc_of", "rr_scene_free", "rr_quantize",
            "rr_write_png", "rr_render_scene_from_file", "rr_render_scene_from_file_devices", "rr_create_multi",
            "rr_rccl_unique_id", "rr_create_rank", "rr_context_info", "rr_render_gather_device", "rr_create_virtual",
-           "rr_unshuffle_host", "rr_stage_row_offset", "rr_build_digest"]
+           "rr_unshuffle_host", "rr_stage_row_offset", "rr_build_digest", "rr_balance_bands", "rr_group_bands",
+           "rr_group_set_bands"]
 RCCL_ID_BYTES = 128
 
 _lib = None
@@ -135,6 +138,9 @@ def lib():
     L.rr_render_gather_device.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(RenderOpts), C.c_void_p,
                                           C.c_void_p]
     L.rr_build_digest.restype = C.c_char_p
+    L.rr_balance_bands.argtypes = [_D, C.c_int64, C.c_int32, C.c_double, C.c_int32, C.POINTER(C.c_int64)]
+    L.rr_group_bands.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.c_int32]
+    L.rr_group_set_bands.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.c_int32]
     _lib = L
     return L
 

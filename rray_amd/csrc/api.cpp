@@ -81,6 +81,7 @@ struct rr_ctx {
         int64_t hs, lrows;
         int32_t aa, part, nparts, block_rows;
         int32_t pw, pad;
+        int32_t row0, pad2;
     } tile_key{};
     bool tiles_valid = false;
     // level-0 launch order of one-batch fused frames: every wave stores its tile's cost (clock cycles) and the
@@ -89,6 +90,7 @@ struct rr_ctx {
     int64_t order_tiles = 0;  // the layout the order was built for (tiles; key below)
     TileKey order_key{};
     bool order_valid = false;
+    uint32_t perm_tail[3] = {0, 0, 0};  // the order's entries past the last tile (their own indices), copied from here
     int order_age = 0;
     std::vector<DBuf> comb, comb_ext, pend;  // one per level (comb_ext: scenes with transparency)
     unsigned long long* h_counters = nullptr;
@@ -144,7 +146,18 @@ int check_opts(const rr_camera* cam, const rr_render_opts* o) {
     if (cam->hsize <= 0 || cam->vsize <= 0 || cam->hsize % o->aa || cam->vsize % o->aa)
         return fail(RR_E_ARG, "camera size must be a positive multiple of aa");
     if (cam->hsize > (1ll << 31) || cam->vsize > (1ll << 31)) return fail(RR_E_LIMIT, "camera too large");
+    if (o->row_begin != 0 || o->row_end != 0) {  // a band of output rows (ABI 10)
+        if (o->part != 0 || o->nparts != 1) return fail(RR_E_ARG, "a band (row_begin / row_end) is part 0 of 1");
+        if (o->row_begin < 0 || o->row_end <= o->row_begin || o->row_end > cam->vsize / o->aa)
+            return fail(RR_E_ARG, "band rows out of range: need 0 <= row_begin < row_end <= height");
+    }
     return RR_OK;
+}
+
+// output rows of the part (interleaved blocks) or band (rr_render_opts row_begin / row_end)
+int64_t opts_rows(const rr_render_opts* o, int64_t H) {
+    if (o->row_begin != 0 || o->row_end != 0) return (int64_t)o->row_end - o->row_begin;
+    return rr::part_rows_count(H, o->part, o->nparts, o->block_rows > 0 ? o->block_rows : 8);
 }
 
 rr::DevCamera dev_camera(const rr_camera* c) {
@@ -286,6 +299,7 @@ int tile_bundles(rr_ctx* c, const rr::LevelArgs& base_args, hipStream_t st, cons
     key.nparts = T.nparts;
     key.block_rows = T.block_rows;
     key.pw = T.pw;
+    key.row0 = T.row0;
     if (!c->tiles_valid || std::memcmp(&key, &c->tile_key, sizeof key) != 0) {
         if (T.pw)
             HIPCHK(rr::launch_pixel_wave_bundles(T, c->tiles.as<float>(), n_tiles, st));
@@ -398,18 +412,23 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
     set_level0_index(T0);
     // chain frames order their camera waves too (tiles or pixel waves; the chains' depths spread tile costs widely)
     const int64_t n_tiles = T0.pw ? pixel_waves(T0) : T0.tile_fast ? T0.hs * T0.lrows / 64 : 0;
-    const bool order_ok = (fused || tree) && !c->S.general && B >= total && n_tiles > 0 && n_tiles < ((int64_t)1 << 31) &&
-                          n_tiles % 4 == 0 &&  // whole launch blocks (the group order permutes a block's four tiles)
-                          (T0.pw || n_tiles * 64 == total) &&
-                          ((c->S.has_groups && (k == 0 || max_depth == 0)) || (chain && !std::getenv("RRAY_NO_CHAIN_ORDER")));
     // the order's unit: single waves, so a block's four waves cost alike (the costliest first) and the block's
     // resources free together.  Groups of a block's four adjacent tiles (RRAY_ORDER_GROUP=4: their output rows join
     // into whole cache lines) measured slower: C3 6.33 vs 7.17 ms, C4 0.510 vs 0.520 ms, C5 equal
     int order_group = 1;
     if (const char* g = std::getenv("RRAY_ORDER_GROUP")) order_group = std::atoi(g) == rr::RR_ORDER_GROUP ? rr::RR_ORDER_GROUP : 1;
+    const bool order_ok = (fused || tree) && !c->S.general && B >= total && n_tiles > 0 && n_tiles < ((int64_t)1 << 31) &&
+                          (order_group == 1 || n_tiles % 4 == 0) &&  // the group order permutes a block's four tiles
+                          (T0.pw || n_tiles * 64 == total) &&
+                          ((c->S.has_groups && (k == 0 || max_depth == 0)) || (chain && !std::getenv("RRAY_NO_CHAIN_ORDER")));
+    // the launch's last block may hold up to three wave slots past the last tile (n_tiles not a multiple of 4: a
+    // pixel-wave part of 270 output rows has 148 230 waves): the order and cost arrays run to whole blocks, the extra
+    // slots' order entries are their own indices (their lanes are past the launch's samples and do nothing but record
+    // a cost nobody sorts).  Until round 6 such layouts ran unordered: C3's 8-part rows among them.
+    const int64_t n_pad = (n_tiles + 3) & ~(int64_t)3;
     if (order_ok) {
-        HIPCHK(c->tile_cost.ensure((size_t)n_tiles * sizeof(uint32_t)));
-        HIPCHK(c->tile_perm.ensure((size_t)n_tiles * sizeof(uint32_t)));
+        HIPCHK(c->tile_cost.ensure((size_t)n_pad * sizeof(uint32_t)));
+        HIPCHK(c->tile_perm.ensure((size_t)n_pad * sizeof(uint32_t)));
         HIPCHK(c->tile_hist.ensure(256 * sizeof(uint32_t)));
         rr_ctx::TileKey key{};  // the layout only: a camera change keeps the order (costs stay a good guess)
         key.hs = T0.hs;
@@ -419,12 +438,18 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
         key.nparts = T0.nparts;
         key.block_rows = T0.block_rows;
         key.pw = T0.pw;
+        key.row0 = T0.row0;
         key.pad = (chain ? 1 : 0) | (order_group == 1 ? 2 : 0);  // chain and level-0-only frames of one layout, and
                                                                   // each order unit, keep orders of their own
         if (c->order_tiles != n_tiles || std::memcmp(&key, &c->order_key, sizeof key) != 0) {
             c->order_valid = false;
             c->order_tiles = n_tiles;
             c->order_key = key;
+            if (n_pad > n_tiles) {  // the identity for the slots past the last tile
+                for (int64_t t = n_tiles; t < n_pad; ++t) c->perm_tail[t - n_tiles] = (uint32_t)t;
+                HIPCHK(hipMemcpyAsync(c->tile_perm.as<uint32_t>() + n_tiles, c->perm_tail,
+                                      (size_t)(n_pad - n_tiles) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+            }
         }
         // a layout's first frame: order by a guess from the camera bundles (launch order left the first frame's
         // slowest tiles last: C4 0.59 vs 0.51 ms), and re-sort by the measured costs right after it
@@ -440,7 +465,8 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
         const int64_t nb = std::min(B, total - base);
         const LevelPlan p = plan_levels(nb, k, plan_depth, ext, fused);
         // per-level queue counters [level][LC_*], zeroed once per batch (appends, pending, n1/n2 lists)
-        if (p.levels > 1 || ext)
+        // (the in-wave chains and trees use none: no memset in their frames, which cost a C1 frame 9.6 us as two fills)
+        if (p.levels > 1 || (ext && !tree))
             HIPCHK(hipMemsetAsync(lc, 0, (size_t)p.levels * rr::LC_COUNT * sizeof(unsigned int), st));
         if (spill) HIPCHK(hipMemsetAsync(c->deep_count.p, 0, (size_t)deep_nseg * sizeof(unsigned int), st));
         for (int d = 0; d < p.levels; ++d) {
@@ -649,8 +675,7 @@ int render_validate(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o) {
     if (!c->has_scene) return fail(RR_E_ARG, "no scene uploaded");
     int rc = check_opts(cam, o);
     if (rc != RR_OK) return rc;
-    const int32_t block = o->block_rows > 0 ? o->block_rows : 8;
-    const int64_t rows = part_rows_count(cam->vsize / o->aa, o->part, o->nparts, block);
+    const int64_t rows = opts_rows(o, cam->vsize / o->aa);
     if (rows * o->aa * cam->hsize >= ((int64_t)1 << 31))
         return fail(RR_E_LIMIT, "a part must hold fewer than 2^31 samples (use more parts)");
     return RR_OK;
@@ -978,7 +1003,7 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     HIPCHK(hipSetDevice(c->device));
     const int32_t block = o->block_rows > 0 ? o->block_rows : 8;
     const int64_t H = cam->vsize / o->aa, W = cam->hsize / o->aa;
-    const int64_t rows = rr::part_rows_count(H, o->part, o->nparts, block);
+    const int64_t rows = opts_rows(o, H);
     const int64_t local_rows = rows * o->aa;
     const int64_t total = local_rows * cam->hsize;
     // Everything is enqueued on the caller's stream (no cross-stream events per call: a HIP event
@@ -1012,6 +1037,7 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     A.part = o->part;
     A.nparts = o->nparts;
     A.block_rows = block;
+    A.row0 = o->row_begin;  // 0 unless a band (check_opts)
     A.rays0 = nullptr;
     A.seed = o->seed;
     A.jitter_mode = o->jitter_mode;
@@ -1098,9 +1124,8 @@ int rr_render(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, double* 
     if (c->group) return rr::group_render(c->group, cam, o, out_canvas, out_avg, stats);
     int rc = check_opts(cam, o);
     if (rc != RR_OK) return rc;
-    const int32_t block = o->block_rows > 0 ? o->block_rows : 8;
     const int64_t H = cam->vsize / o->aa, W = cam->hsize / o->aa;
-    const int64_t rows = rr::part_rows_count(H, o->part, o->nparts, block);
+    const int64_t rows = opts_rows(o, H);
     const int64_t total = rows * o->aa * cam->hsize;
     HIPCHK(hipSetDevice(c->device));
     const bool want_avg = (o->flags & RR_OUT_AVG) && out_avg;
@@ -1191,3 +1216,24 @@ int rr_is_shadowed(rr_ctx* c, int64_t n, const double* points, const double* lig
 }
 
 }  // extern "C"
+
+// ---- ABI 10: cost-balanced bands (multi.cpp) ----
+extern "C" int rr_balance_bands(const double* row_cost, int64_t height, int32_t nparts, double root_extra, int32_t align,
+                                int64_t* bounds) {
+    if (!row_cost || !bounds || height < 1 || nparts < 1 || align < 1)
+        return fail(RR_E_ARG, "rr_balance_bands: need row costs, height >= 1, nparts >= 1, align >= 1");
+    rr::balance_bands(row_cost, height, nparts, root_extra, align, bounds);
+    return RR_OK;
+}
+
+extern "C" int rr_group_bands(rr_ctx* c, int64_t* bounds, int32_t n) {
+    if (!c || !bounds) return fail(RR_E_ARG, "null argument");
+    if (!c->group) return fail(RR_E_ARG, "rr_group_bands: not a multi-device context");
+    return rr::group_bands(c->group, bounds, n);
+}
+
+extern "C" int rr_group_set_bands(rr_ctx* c, const int64_t* bounds, int32_t n) {
+    if (!c || !bounds) return fail(RR_E_ARG, "null argument");
+    if (!c->group) return fail(RR_E_ARG, "rr_group_set_bands: not a multi-device context");
+    return rr::group_set_bands(c->group, bounds, n);
+}

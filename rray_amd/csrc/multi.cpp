@@ -109,6 +109,12 @@ struct rr_group {
     std::vector<DevMem> tile[2];          // per local part: its tile (rows of the part, in tile order)
     DevMem frame;                         // root: assembled frame for the blocking rr_render
     DevMem stage;                         // root: every part's tile back to back (part p at stage_row_offset(p))
+    // band partition (the default): rank p renders output rows [bands[p], bands[p + 1]); calibrated on the first band
+    // frame of a layout (calibrate_bands) or imposed by rr_group_set_bands
+    std::vector<int64_t> bands;
+    int64_t band_w = -1, band_h = -1;     // the layout the bands were made for
+    int32_t band_aa = -1;
+    DevMem dbounds;                       // rank processes: the bounds' device copy for the broadcast
     int64_t k = 0;                        // frames issued (buffer and render context = k % 2)
     int nlocal() const { return (int)devices.size(); }
     int last() const { return k > 0 ? (int)((k - 1) & 1) : 0; }  // the set that rendered the latest frame
@@ -298,6 +304,7 @@ void group_destroy(rr_group* g) {
         for (int b = 0; b < 2; ++b)
             if (l < g->render_st[b].size() && g->render_st[b][l]) (void)hipStreamDestroy(g->render_st[b][l]);
         if (l < g->comm_st.size() && g->comm_st[l]) (void)hipStreamDestroy(g->comm_st[l]);
+        if (l == 0) g->dbounds.release();
         if (l == 0 && g->root_here()) {
             g->frame.release();
             g->stage.release();
@@ -398,11 +405,198 @@ static int enqueue_frame(rr_group* g, const rr_camera* cam, const std::vector<rr
     return RR_OK;
 }
 
+// Cost-balanced bands for this layout.  Rank 0 measures the frame's cost per row on its own device: the frame as 16
+// bands of equal height (multiples of 8 rows), each rendered three times on one context and the third render timed
+// with events (the first renders of a layout build its camera bundles and run in a guessed wave order; a part renders
+// its band over and over), which gives a per-row profile; rr_balance_bands cuts it into N bands, with rank 0's own
+// transfer work added to its band (a device copy of the frame, timed: rank 0 writes the other parts' incoming rows and
+// copies its own, beside its render).  Two refinements then time each of the N bands the same way and rescale the
+// profile inside it to the measured time before cutting again: 16 equal bands are not additive (a band's time is not
+// the sum of its rows' shares: launch tails, and the cost order of a small launch), the N bands are what the parts
+// will render.  A process group gets the bounds from rank 0 by one ncclBroadcast — the only collective besides the
+// frames' transfers, once per layout.  Every rank calls this for the same frame (the layout is an argument every rank
+// passes alike).
+static int calibrate_bands(rr_group* g, const rr_camera* cam, const rr_render_opts* o, int64_t W, int64_t H) {
+    const int N = g->nranks;
+    const int64_t row = W * 3;
+    std::vector<int64_t> b(N + 1, 0);
+    group_drain(g);  // a layout change: nothing of the previous frames may still use the buffers below
+    if (g->root_here()) {
+        GHIP(hipSetDevice(g->devices[0]));
+        rr_ctx* c = g->subs[0][0];
+        hipStream_t st = g->render_st[0][0];
+        GHIP(g->stage.ensure((size_t)H * (size_t)row * sizeof(double)));
+        GHIP(g->frame.ensure((size_t)H * (size_t)row * sizeof(double)));
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        GHIP(hipEventCreate(&e0));
+        GHIP(hipEventCreate(&e1));
+        // rows [y0, y1): three renders, the third timed
+        const auto time_band = [&](int64_t y0, int64_t y1, float& ms) -> int {
+            rr_render_opts so = *o;
+            so.part = 0;
+            so.nparts = 1;
+            so.row_begin = (int32_t)y0;
+            so.row_end = (int32_t)y1;
+            so.flags = RR_OUT_AVG | RR_NO_FRAME_TIMING;
+            double* out = static_cast<double*>(g->stage.p) + y0 * row;
+            for (int k = 0; k < 3; ++k) {
+                if (k == 2) GHIP(hipEventRecord(e0, st));
+                int rc = rr_render_device(c, cam, &so, nullptr, out, st);
+                if (rc != RR_OK) return rc;
+            }
+            GHIP(hipEventRecord(e1, st));
+            GHIP(hipEventSynchronize(e1));
+            GHIP(hipEventElapsedTime(&ms, e0, e1));
+            return RR_OK;
+        };
+        int rc = RR_OK;
+        std::vector<double> cost(H, 0.0);
+        const int64_t nb = std::min<int64_t>(16, (H + 7) / 8);
+        const int64_t hb = ((H + nb - 1) / nb + 7) / 8 * 8;
+        for (int64_t y0 = 0; y0 < H && rc == RR_OK; y0 += hb) {
+            const int64_t y1 = std::min<int64_t>(H, y0 + hb);
+            float ms = 0.0f;
+            rc = time_band(y0, y1, ms);
+            for (int64_t y = y0; y < y1; ++y) cost[y] = (double)ms / (double)(y1 - y0);
+        }
+        double extra = 0.0;
+        if (rc == RR_OK && N > 1) {
+            float copy_ms = 0.0f;
+            GHIP(hipEventRecord(e0, st));
+            GHIP(hipMemcpyAsync(g->frame.p, g->stage.p, (size_t)H * (size_t)row * sizeof(double), hipMemcpyDeviceToDevice,
+                                st));
+            GHIP(hipEventRecord(e1, st));
+            GHIP(hipEventSynchronize(e1));
+            GHIP(hipEventElapsedTime(&copy_ms, e0, e1));
+            // a copy reads and writes every byte: the incoming (N - 1) / N of the frame is written once, the own band
+            // (about 1 / N of it) read and written
+            extra = (double)copy_ms * (0.5 * (double)(N - 1) / N + 1.0 / N);
+        }
+        if (rc == RR_OK) balance_bands(cost.data(), H, N, extra, 8, b.data());
+        for (int it = 0; it < 2 && rc == RR_OK && N > 1; ++it) {
+            for (int p = 0; p < N && rc == RR_OK; ++p) {
+                if (b[p + 1] <= b[p]) continue;
+                float ms = 0.0f;
+                rc = time_band(b[p], b[p + 1], ms);
+                double sum = 0.0;
+                for (int64_t y = b[p]; y < b[p + 1]; ++y) sum += cost[y];
+                if (rc == RR_OK && sum > 0.0)
+                    for (int64_t y = b[p]; y < b[p + 1]; ++y) cost[y] *= (double)ms / sum;
+            }
+            if (rc == RR_OK) balance_bands(cost.data(), H, N, extra, 8, b.data());
+        }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        if (rc != RR_OK) return rc;
+        trace("calibrate_bands %p: %lld x %lld, %d parts, band 0 = %lld rows, extra %.4f ms", (void*)g, (long long)W,
+              (long long)H, N, (long long)b[1], extra);
+    }
+    if (!g->virt && g->nlocal() < N) {  // one process per GPU: rank 0's bounds to every rank
+        GHIP(hipSetDevice(g->devices[0]));
+        GHIP(g->dbounds.ensure((size_t)(N + 1) * sizeof(int64_t)));
+        if (g->root_here())
+            GHIP(hipMemcpy(g->dbounds.p, b.data(), (size_t)(N + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+        GNCCL(ncclBroadcast(g->dbounds.p, g->dbounds.p, (size_t)(N + 1), ncclInt64, 0, g->comms[0], g->comm_st[0]));
+        GHIP(hipStreamSynchronize(g->comm_st[0]));
+        GHIP(hipMemcpy(b.data(), g->dbounds.p, (size_t)(N + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+    }
+    g->bands = b;
+    g->band_w = W;
+    g->band_h = H;
+    g->band_aa = o->aa;
+    return RR_OK;
+}
+
+// One band frame: every local part renders its band into its tile buffer; rank 0 receives the other parts' tiles
+// straight into their frame rows (one ncclRecv per part) and copies its own there; a virtual group copies every
+// tile into its rows on the root's transfer stream in place of the send / receive pairs.  `enqueued` as enqueue_frame.
+static int enqueue_frame_bands(rr_group* g, const rr_camera* cam, const std::vector<rr_render_opts>& opts, double* frame,
+                               hipStream_t caller, int64_t W, int b, bool& enqueued) {
+    const int n = g->nlocal();
+    const int64_t row = W * 3;
+    const auto rows_of = [&](int p) { return g->bands[p + 1] - g->bands[p]; };
+    for (int l = 0; l < n; ++l) {
+        GHIP(hipSetDevice(g->devices[l]));
+        GHIP(hipStreamWaitEvent(g->render_st[b][l], g->ev_gathered[b][l], 0));
+        enqueued = true;
+        if (rows_of(g->rank0 + l) > 0) {
+            int rc = rr_render_device(g->subs[b][l], cam, &opts[l], nullptr, g->tile[b][l].p, g->render_st[b][l]);
+            if (rc != RR_OK) return rc;
+        }
+        if (l == g->fail_after) return gfail(RR_E_HIP, "injected failure after part " + std::to_string(l) + "'s render");
+        GHIP(hipEventRecord(g->ev_rendered[b][l], g->render_st[b][l]));
+        GHIP(hipStreamWaitEvent(g->gather_stream(l), g->ev_rendered[b][l], 0));
+    }
+    if (g->root_here()) {
+        GHIP(hipSetDevice(g->devices[0]));
+        // the frame is written in the caller's stream order: the copies and receives into it wait for the caller
+        if (caller) GHIP(hipStreamWaitEvent(g->comm_st[0], g->ev_caller, 0));
+    }
+    if (g->virt) {
+        GHIP(hipSetDevice(g->devices[0]));
+        for (int l = 0; l < n; ++l)
+            if (rows_of(l) > 0)
+                GHIP(hipMemcpyAsync(frame + g->bands[l] * row, g->tile[b][l].p, (size_t)(rows_of(l) * row) * sizeof(double),
+                                    hipMemcpyDeviceToDevice, g->comm_st[0]));
+    } else {
+        if (g->root_here() && rows_of(0) > 0) {
+            GHIP(hipSetDevice(g->devices[0]));
+            GHIP(hipMemcpyAsync(frame, g->tile[b][0].p, (size_t)(rows_of(0) * row) * sizeof(double), hipMemcpyDeviceToDevice,
+                                g->comm_st[0]));
+        }
+        ncclResult_t r = ncclGroupStart();
+        if (r == ncclSuccess) {
+            for (int l = 0; l < n && r == ncclSuccess; ++l) {
+                const int p = g->rank0 + l;
+                if (p != 0 && rows_of(p) > 0)
+                    r = ncclSend(g->tile[b][l].p, (size_t)(rows_of(p) * row), ncclFloat64, 0, g->comms[l], g->comm_st[l]);
+                if (!(g->root_here() && l == 0)) continue;
+                for (int32_t q = 1; q < g->nranks && r == ncclSuccess; ++q)
+                    if (rows_of(q) > 0)
+                        r = ncclRecv(frame + g->bands[q] * row, (size_t)(rows_of(q) * row), ncclFloat64, q, g->comms[0],
+                                     g->comm_st[0]);
+            }
+            const ncclResult_t e = ncclGroupEnd();
+            if (r == ncclSuccess) r = e;
+        }
+        if (r != ncclSuccess) return gfail(RR_E_HIP, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
+    }
+    for (int l = 0; l < n; ++l) {  // a virtual group's tiles are all read on comm_st[0]
+        GHIP(hipSetDevice(g->devices[l]));
+        GHIP(hipEventRecord(g->ev_gathered[b][l], g->gather_stream(l)));
+    }
+    if (g->root_here() && caller) {
+        GHIP(hipSetDevice(g->devices[0]));
+        GHIP(hipStreamWaitEvent(caller, g->ev_gathered[b][0], 0));
+    }
+    return RR_OK;
+}
+
+int group_bands(rr_group* g, int64_t* bounds, int32_t n) {
+    if (g->bands.empty()) return 0;
+    if (n < g->nranks + 1) return gfail(RR_E_ARG, "rr_group_bands: need nranks + 1 values");
+    std::copy(g->bands.begin(), g->bands.end(), bounds);
+    return g->nranks + 1;
+}
+
+int group_set_bands(rr_group* g, const int64_t* bounds, int32_t n) {
+    if (n != g->nranks + 1) return gfail(RR_E_ARG, "rr_group_set_bands: need nranks + 1 bounds");
+    if (bounds[0] != 0) return gfail(RR_E_ARG, "rr_group_set_bands: bounds[0] must be 0");
+    for (int32_t p = 0; p < g->nranks; ++p)
+        if (bounds[p + 1] < bounds[p]) return gfail(RR_E_ARG, "rr_group_set_bands: bounds must not decrease");
+    group_drain(g);
+    g->bands.assign(bounds, bounds + n);
+    g->band_h = bounds[n - 1];
+    g->band_w = 0;  // any width and aa of that height (checked per frame)
+    g->band_aa = 0;
+    return RR_OK;
+}
+
 int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts* o, void* d_frame, void* stream) {
     DeviceGuard device_guard;
     if (!cam || !o) return gfail(RR_E_ARG, "null camera/options");
-    if (o->nparts != 1 || o->part != 0)
-        return gfail(RR_E_ARG, "a multi-device context splits the whole frame itself: pass part 0 of 1");
+    if (o->nparts != 1 || o->part != 0 || o->row_begin != 0 || o->row_end != 0)
+        return gfail(RR_E_ARG, "a multi-device context splits the whole frame itself: pass part 0 of 1, no band");
     if (o->flags & (RR_OUT_CANVAS | RR_OUT_AVG_F32))
         return gfail(RR_E_ARG, "multi-device contexts produce the f64 AA-averaged image only (RR_OUT_AVG)");
     if (o->aa < 1 || cam->hsize <= 0 || cam->vsize <= 0 || cam->hsize % o->aa || cam->vsize % o->aa)
@@ -412,21 +606,41 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
     const int64_t W = cam->hsize / o->aa, H = cam->vsize / o->aa, row = W * 3;
     const int b = (int)(g->k & 1);
     const int n = g->nlocal();
+    const bool interleave = (o->flags & RR_PART_INTERLEAVE) != 0;
+    if (!interleave && (g->bands.empty() || g->band_h != H ||
+                        (g->band_w != 0 && (g->band_w != W || g->band_aa != o->aa)))) {
+        int rc = calibrate_bands(g, cam, o, W, H);
+        if (rc != RR_OK) return rc;
+    }
     // every part's options and buffers are checked / allocated before any work is enqueued: a failure
     // here returns before this rank joins the collective, never between its render and its transfer
     std::vector<rr_render_opts> opts(n, *o);
     for (int l = 0; l < n; ++l) {
         rr_render_opts& so = opts[l];
-        so.part = g->rank0 + l;
-        so.nparts = g->nranks;
-        so.block_rows = block;
+        const int p = g->rank0 + l;
+        int64_t rows;
+        if (interleave) {
+            so.part = p;
+            so.nparts = g->nranks;
+            so.block_rows = block;
+            rows = part_rows_count(H, so.part, g->nranks, block);
+        } else {  // the band [bands[p], bands[p + 1])
+            so.part = 0;
+            so.nparts = 1;
+            so.block_rows = block;
+            so.row_begin = (int32_t)g->bands[p];
+            so.row_end = (int32_t)g->bands[p + 1];
+            rows = g->bands[p + 1] - g->bands[p];
+        }
         so.flags = RR_OUT_AVG | (o->flags & RR_NO_FRAME_TIMING);
-        int rc = render_validate(g->subs[b][l], cam, &so);
-        if (rc != RR_OK) return rc;
+        if (rows > 0) {
+            int rc = render_validate(g->subs[b][l], cam, &so);
+            if (rc != RR_OK) return rc;
+        }
         GHIP(hipSetDevice(g->devices[l]));
-        GHIP(g->tile[b][l].ensure((size_t)part_rows_count(H, so.part, g->nranks, block) * (size_t)row * sizeof(double)));
+        GHIP(g->tile[b][l].ensure((size_t)rows * (size_t)row * sizeof(double)));
     }
-    if (g->root_here()) {  // the staging buffer (the whole frame's rows), before any work is enqueued
+    if (g->root_here() && interleave) {  // the staging buffer (the whole frame's rows), before any work is enqueued
         GHIP(hipSetDevice(g->devices[0]));
         GHIP(g->stage.ensure((size_t)H * (size_t)row * sizeof(double)));
     }
@@ -438,7 +652,8 @@ int group_render_gather(rr_group* g, const rr_camera* cam, const rr_render_opts*
     bool enqueued = false;
     trace("group_render_gather %p: frame %lld, %d parts, %lld x %lld, block %d", (void*)g, (long long)g->k, n,
           (long long)W, (long long)H, block);
-    const int rc = enqueue_frame(g, cam, opts, static_cast<double*>(d_frame), caller, W, H, block, b, enqueued);
+    const int rc = interleave ? enqueue_frame(g, cam, opts, static_cast<double*>(d_frame), caller, W, H, block, b, enqueued)
+                              : enqueue_frame_bands(g, cam, opts, static_cast<double*>(d_frame), caller, W, b, enqueued);
     if (rc != RR_OK) {
         trace("group_render_gather %p: error %d after %s: %s", (void*)g, rc, enqueued ? "enqueuing" : "no work",
               rr_last_error());
@@ -468,7 +683,7 @@ int group_render(rr_group* g, const rr_camera* cam, const rr_render_opts* o, dou
         GHIP(g->frame.ensure((size_t)W * H * 3 * sizeof(double)));
     }
     rr_render_opts so = *o;
-    so.flags = RR_OUT_AVG;
+    so.flags = RR_OUT_AVG | (o->flags & RR_PART_INTERLEAVE);
     int rc = group_render_gather(g, cam, &so, g->root_here() ? g->frame.p : nullptr, nullptr);
     if (rc != RR_OK) return rc;
     trace("group_render %p: synchronise", (void*)g);

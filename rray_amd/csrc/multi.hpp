@@ -30,6 +30,9 @@ rr_ctx* group_local(rr_group* g, int l);  // local device context l (0 = the low
 int group_kernel_profile(rr_group* g, int enable);
 int group_kernel_times(rr_group* g, double* ms, uint64_t* launches, int32_t n);
 int group_info(const rr_group* g, int32_t* nranks, int32_t* rank0, int32_t* nlocal);
+// the band bounds (rr_group_bands / rr_group_set_bands)
+int group_bands(rr_group* g, int64_t* bounds, int32_t n);
+int group_set_bands(rr_group* g, const int64_t* bounds, int32_t n);
 // api.cpp: every argument check of rr_render_device, without enqueueing anything
 int render_validate(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o);
 

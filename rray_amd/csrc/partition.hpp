@@ -53,4 +53,32 @@ inline void for_each_part_run(int64_t height, int32_t part, int32_t nparts, int3
         f(j, frame_row_of(j, part, nparts, block), rows - j < block ? rows - j : (int64_t)block);
 }
 
+// Cost-balanced contiguous bands (the multi-device default, multi.cpp): bounds[0] = 0 <= ... <= bounds[nparts] =
+// height such that part p's cost — the sum of row_cost over its rows, plus root_extra for part 0 (rank 0's transfer
+// work, which runs beside its render) — is as even as `align` allows.  Each inner bound is the row where the
+// cumulative cost (root_extra counted first) crosses p / nparts of the total, interpolated within the row and rounded
+// to the nearest multiple of align, kept monotone.  Host only.
+inline void balance_bands(const double* row_cost, int64_t height, int32_t nparts, double root_extra, int32_t align,
+                          int64_t* bounds) {
+    const auto cost = [&](int64_t y) { return row_cost[y] > 0.0 ? row_cost[y] : 0.0; };  // NaN and negatives count 0
+    const double extra = root_extra > 0.0 ? root_extra : 0.0;
+    double total = extra;
+    for (int64_t y = 0; y < height; ++y) total += cost(y);
+    bounds[0] = 0;
+    int64_t y = 0;
+    double acc = extra;  // cost of rows [0, y) plus the root's extra
+    for (int32_t p = 1; p < nparts; ++p) {
+        const double target = total * (double)p / (double)nparts;
+        while (y < height && acc + cost(y) <= target) acc += cost(y++);
+        // the crossing lies in row y: the fraction of it that completes the target
+        double at = (double)y;
+        if (y < height && cost(y) > 0.0) at += (target - acc) / cost(y);
+        int64_t b = (int64_t)(at / align + 0.5) * align;
+        if (b > height) b = height;
+        if (b < bounds[p - 1]) b = bounds[p - 1];
+        bounds[p] = b;
+    }
+    bounds[nparts] = height;
+}
+
 }  // namespace rr

@@ -250,6 +250,16 @@ def unshuffle(staged, height, nparts, block_rows=8):
     return frame
 
 
+def balance_bands(row_cost, nparts, root_extra=0.0, align=8):
+    """rr_balance_bands: band bounds (nparts + 1) over len(row_cost) rows with even cost per band, part 0 carrying
+    root_extra on top, inner bounds multiples of align."""
+    c = np.ascontiguousarray(row_cost, np.float64)
+    out = np.zeros(nparts + 1, np.int64)
+    check(lib().rr_balance_bands(_dp(c), len(c), nparts, float(root_extra), align,
+                                 out.ctypes.data_as(C.POINTER(C.c_int64))))
+    return out
+
+
 def device_count():
     n = C.c_int(0)
     lib().rr_device_count(C.byref(n))
@@ -310,6 +320,21 @@ class Renderer:
         check(lib().rr_render_gather_device(self.h, C.byref(cam), C.byref(opts), C.c_void_p(d_frame) if d_frame else None,
                                             C.c_void_p(stream) if stream else None))
 
+    def bands(self):
+        """rr_group_bands: the band bounds of a multi-device context (nranks + 1 rows), or None before its first
+        band frame calibrated them."""
+        nranks = self.info()[0]
+        out = (C.c_int64 * (nranks + 1))()
+        n = lib().rr_group_bands(self.h, out, nranks + 1)
+        if n < 0:
+            check(n)
+        return list(out) if n else None
+
+    def set_bands(self, bounds):
+        """rr_group_set_bands: impose the band bounds (every rank the same)."""
+        b = (C.c_int64 * len(bounds))(*bounds)
+        check(lib().rr_group_set_bands(self.h, b, len(bounds)))
+
     def close(self):
         if getattr(self, "h", None):
             lib().rr_destroy(self.h)
@@ -327,12 +352,15 @@ class Renderer:
         self._scene = scene
 
     def render(self, cam, aa=1, max_depth=5, seed=0, jitter_mode=0, part=0, nparts=1, block_rows=8, canvas=False,
-               avg=True):
-        """Camera::render -> dict(avg=(rows, W, 3) f64 before `as u8`, canvas=(rows*aa, W*aa, 3), stats)."""
+               avg=True, band=None, interleave=False):
+        """Camera::render -> dict(avg=(rows, W, 3) f64 before `as u8`, canvas=(rows*aa, W*aa, 3), stats).
+        band=(row_begin, row_end): only those output rows (ABI 10); interleave: a multi-device context splits the
+        frame in interleaved tiles (RR_PART_INTERLEAVE) instead of cost-balanced bands."""
         o = _lib.RenderOpts(aa, max_depth, seed, jitter_mode, part, nparts, block_rows,
-                            (_lib.RR_OUT_CANVAS if canvas else 0) | (_lib.RR_OUT_AVG if avg else 0))
+                            (_lib.RR_OUT_CANVAS if canvas else 0) | (_lib.RR_OUT_AVG if avg else 0) |
+                            (_lib.RR_PART_INTERLEAVE if interleave else 0), *(band or (0, 0)))
         H, W = cam.vsize // aa, cam.hsize // aa
-        rows = len(part_rows(H, part, nparts, block_rows))
+        rows = max(band[1] - band[0], 0) if band else len(part_rows(H, part, nparts, block_rows))
         out_avg = np.zeros((rows, W, 3), np.float64) if avg else None
         out_canvas = np.zeros((rows * aa, cam.hsize, 3), np.float64) if canvas else None
         st = _lib.Stats()

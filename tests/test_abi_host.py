@@ -449,3 +449,32 @@ def test_cli_argument_errors():
     assert r.returncode == 1 and "File does not exist" in r.stderr
     r = subprocess.run([cli, "-V"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and r.stdout.startswith("rray")
+
+
+def test_balance_bands():
+    """rr_balance_bands (ABI 10, partition.hpp balance_bands): the multi-device bands from per-row costs — bounds from 0
+    to height, non-decreasing, inner bounds on `align` rows; equal costs give equal bands; a costly region gets thinner
+    bands; rank 0's extra (its transfer work) shrinks band 0 by about that much cost; degenerate inputs stay valid."""
+    import rray_amd as R
+
+    b = R.balance_bands(np.ones(2160), 8)  # the even split 270 p, on 8-row boundaries
+    assert b[0] == 0 and b[-1] == 2160 and all(x % 8 == 0 and abs(x - 270 * p) <= 4 for p, x in enumerate(b[:-1]))
+    cost = np.ones(800)
+    cost[400:] = 3.0  # the lower half three times as costly
+    b = R.balance_bands(cost, 4)
+    assert b[0] == 0 and b[-1] == 800 and all(x % 8 == 0 for x in b[:-1])
+    sums = [cost[b[p]:b[p + 1]].sum() for p in range(4)]
+    assert max(sums) - min(sums) <= 8 * 3.0  # within one aligned block of the most costly rows
+    b0 = R.balance_bands(np.ones(2160), 8, root_extra=80.0)
+    assert 0 < b0[1] < 270 and abs((b0[1] + 80.0) - (2160 + 80.0) / 8) <= 8
+    big = R.balance_bands(np.ones(64), 4, root_extra=1e6)  # the root's extra outweighs the frame: rank 0 gets no rows
+    assert big[0] == big[1] == 0 and big[-1] == 64
+    z = R.balance_bands(np.zeros(100), 3)  # no cost information: still a valid partition
+    assert z[0] == 0 and z[-1] == 100 and all(x <= y for x, y in zip(z, z[1:]))
+    many = R.balance_bands(np.ones(16), 8)  # more parts than 8-row blocks: some bands empty
+    assert many[0] == 0 and many[-1] == 16 and all(x <= y for x, y in zip(many, many[1:]))
+    nan = np.ones(64)
+    nan[10] = np.nan
+    assert R.balance_bands(nan, 2)[-1] == 64
+    with pytest.raises(R.RRError):
+        R.balance_bands(np.ones(10), 0)

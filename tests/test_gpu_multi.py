@@ -64,12 +64,15 @@ def test_group_context_matches_single_device(R, single, kind):
         g.close()
 
 
+@pytest.mark.parametrize("interleave", [False, True])
 @pytest.mark.parametrize("nparts,block", [(2, 8), (3, 8), (8, 8), (3, 3), (2, 1)])
-def test_virtual_group_assembles_the_frame(R, single, nparts, block):
-    """N virtual ranks (row tiles, each tile's runs placed into their frame rows with nparts = N) reassemble
-    the 1-part image bit for bit.  40 output rows = 5 blocks of 8: not a multiple of 8N for any N here, so
-    parts own different row counts, and at N = 8 three parts own no rows at all; 3-row blocks end in a
-    partial run.  C3's scene (reflection chains, depth 5) at its own AA."""
+def test_virtual_group_assembles_the_frame(R, single, nparts, block, interleave):
+    """N virtual ranks reassemble the 1-part image bit for bit, in both partitions: cost-balanced bands (the default:
+    each part's band copied into its frame rows) and interleaved row tiles (RR_PART_INTERLEAVE: each tile's runs placed
+    into their frame rows with nparts = N).  40 output rows = 5 blocks of 8: not a multiple of 8N for any N here, so
+    parts own different row counts, and at N = 8 three parts own no rows at all (bands: aligned to 8 rows, so at
+    most 5 parts own rows); 3-row blocks end in a partial run.  C3's scene (reflection chains, depth 5) at its own
+    AA."""
     W, H, aa = 48, 40, 3
     scene = _scene(R, "c3_s1024_reflect.yaml", W, H, aa)
     single.upload(scene)
@@ -78,19 +81,71 @@ def test_virtual_group_assembles_the_frame(R, single, nparts, block):
     try:
         assert g.info() == (nparts, 0, nparts)
         g.upload(scene)
-        got = g.render(scene.camera, aa=aa, block_rows=block)
+        got = g.render(scene.camera, aa=aa, block_rows=block, interleave=interleave)
         assert np.array_equal(got["avg"], ref["avg"])
         for k in ("rays", "shadow_rays", "shade_events", "samples"):
             assert got["stats"][k] == ref["stats"][k], k
+        b = g.bands()
+        if interleave:
+            assert b is None
+        else:  # calibrated: 0 .. H, non-decreasing, inner bounds on 8-row boundaries
+            assert b[0] == 0 and b[-1] == H and len(b) == nparts + 1
+            assert all(x <= y for x, y in zip(b, b[1:])) and all(x % 8 == 0 for x in b[:-1])
     finally:
         g.close()
 
 
-@pytest.mark.parametrize("block", [1, 3, 8])
+@pytest.mark.parametrize("bounds", [[0, 0, 16, 40], [0, 8, 8, 40], [0, 40, 40, 40], [0, 13, 27, 40]])
+def test_virtual_group_imposed_bands(R, single, bounds):
+    """rr_group_set_bands: any non-decreasing bounds (empty bands, rank 0 without rows, unaligned bounds) give the
+    1-part image bit for bit through the band transfer, for three frames (both tile buffers and render contexts)."""
+    W, H, aa = 48, 40, 2
+    scene = _scene(R, "c3_s1024_reflect.yaml", W, H, aa)
+    single.upload(scene)
+    ref = single.render(scene.camera, aa=aa)
+    g = R.Renderer.virtual(0, 3)
+    try:
+        g.upload(scene)
+        g.set_bands(bounds)
+        for _ in range(3):
+            got = g.render(scene.camera, aa=aa)
+            assert np.array_equal(got["avg"], ref["avg"])
+        assert g.bands() == bounds
+        with pytest.raises(R.RRError):
+            g.set_bands([0, 20, 10, 40])  # decreasing
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("name,W,H,aa,band", [("c3_s1024_reflect.yaml", 48, 40, 3, (8, 24)),  # pixel waves
+                                              ("c3_s1024_reflect.yaml", 48, 40, 3, (5, 18)),
+                                              ("c4_teapot.yaml", 64, 40, 2, (16, 32)),  # in-wave AA
+                                              ("c4_teapot.yaml", 64, 40, 2, (3, 29)),  # partial tiles
+                                              ("c5_area_light.yaml", 40, 24, 2, (8, 16)),  # jitter keyed by frame rows
+                                              ("c1_readme.yaml", 48, 32, 2, (0, 8)),  # tree kernel
+                                              ("c2_s1024.yaml", 64, 36, 1, (35, 36))])
+def test_band_render_equals_frame_rows(R, single, name, W, H, aa, band):
+    """rr_render_opts row_begin / row_end (ABI 10): a band is those rows of the whole frame bit for bit — camera rays,
+    area-light jitter (keyed by the frame's sample id), recursion counters per row."""
+    scene = _scene(R, name, W, H, aa)
+    single.upload(scene)
+    ref = single.render(scene.camera, aa=aa, canvas=True)
+    got = single.render(scene.camera, aa=aa, band=band, canvas=True)
+    y0, y1 = band
+    assert got["avg"].shape == (y1 - y0, W, 3)
+    assert np.array_equal(got["avg"], ref["avg"][y0:y1])
+    assert np.array_equal(got["canvas"], ref["canvas"][y0 * aa:y1 * aa])
+    assert got["stats"]["samples"] == (y1 - y0) * W * aa * aa
+    with pytest.raises(R.RRError):
+        single.render(scene.camera, aa=aa, band=(y1, y0))
+
+
+@pytest.mark.parametrize("block", [1, 3, 8, 0])
 def test_rccl_group_receives_runs_in_frame_order(R, single, block):
-    """The 1-device RCCL group at several block sizes (40 output rows as 40, 14 or 5 runs of 1, 3 or 8 rows, the
-    last 3-row run partial): the part's tile goes to rank 0 in one ncclSend to itself, is received into the
-    staging buffer and placed into its frame rows, bit for bit the plain context's image."""
+    """The 1-device RCCL group at several block sizes (RR_PART_INTERLEAVE; 40 output rows as 40, 14 or 5 runs of 1, 3
+    or 8 rows, the last 3-row run partial): the part's tile goes to rank 0 in one ncclSend to itself, is received into
+    the staging buffer and placed into its frame rows, bit for bit the plain context's image.  block 0: the band
+    partition (one band: rank 0's own tile copied into the frame, no RCCL operation)."""
     scene = _scene(R, "c3_s1024_reflect.yaml", 48, 40, 1)
     single.upload(scene)
     ref = single.render(scene.camera, aa=1)
@@ -98,7 +153,7 @@ def test_rccl_group_receives_runs_in_frame_order(R, single, block):
     try:
         g.upload(scene)
         for _ in range(2):  # the second frame renders into the other tile buffer and context
-            got = g.render(scene.camera, aa=1, block_rows=block)
+            got = g.render(scene.camera, aa=1, block_rows=block or 8, interleave=block != 0)
             assert np.array_equal(got["avg"], ref["avg"])
     finally:
         g.close()
