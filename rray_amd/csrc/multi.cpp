@@ -1,21 +1,25 @@
-// multi.cpp — multi-device render contexts: row-interleaved tiles, one RCCL transfer per part into a staging
-// buffer, placed into frame order on rank 0.
+// multi.cpp — multi-device render contexts: cost-balanced row bands received straight into rank 0's frame (the
+// default, ABI 10), or row-interleaved tiles through a staging buffer placed into frame order on rank 0
+// (RR_PART_INTERLEAVE).
 //
-// Camera::render (camera.rs:107-121) spreads one frame over every rayon worker; here one frame is
-// spread over GPUs.  Global rank r renders the output rows {y : (y / block) % nranks == r} (the
-// interleaving balances sky and floor cost) as an f64 AA-averaged tile in its own HBM.  Inside one RCCL group
-// per frame every rank sends its whole tile to rank 0 in one ncclSend (over xGMI), and rank 0 receives every
-// part's tile — its own included, as a send to itself — back to back into a staging buffer of `height` rows
-// (part p at partition.hpp stage_row_offset(p)), one ncclRecv per part; one copy kernel per part then places the
-// tile's runs into their frame rows (frame_row_of).  Two tile buffers alternate so that rendering frame k+1
-// overlaps the transfer of frame k: a render waits only for the transfer that last read its buffer.  Each part
-// also alternates between two render contexts (scene copy + level workspace) on two render streams.
+// Camera::render (camera.rs:107-121) spreads one frame over every rayon worker; here one frame is spread over GPUs.
+// Bands (default): global rank r renders the output rows [bands[r], bands[r + 1]) as an f64 AA-averaged tile in its
+// own HBM; the bounds balance the parts' render time (calibrate_bands, once per layout).  Inside one RCCL group per
+// frame every other rank sends its tile to rank 0 in one ncclSend (over xGMI), which rank 0 receives straight into
+// the frame's rows (one ncclRecv per part), and rank 0 copies its own tile there: no staging buffer, no placement.
+// Interleaved (RR_PART_INTERLEAVE): rank r renders the output rows {y : (y / block) % nranks == r}; every rank sends
+// its whole tile to rank 0, which receives each part's tile — its own included, as a send to itself — back to back
+// into a staging buffer of `height` rows (part p at partition.hpp stage_row_offset(p)); one copy kernel per part then
+// places the tile's runs into their frame rows (frame_row_of).  Either way two tile buffers alternate so that
+// rendering frame k+1 overlaps the transfer of frame k (a render waits only for the transfer that last read its
+// buffer), and each part alternates between two render contexts (scene copy + workspace) on two render streams.
 //
 // Three shapes of the same group: rr_create_multi (this process drives n devices, ncclCommInitAll,
 // ncclGroupStart/End around every device's operations), rr_create_rank (one process per GPU, ncclCommInitRank
 // from an id made by rr_rccl_unique_id on rank 0 and shared by the host) and rr_create_virtual (every part on one
-// device, no communicator): a virtual group runs the same staging buffer, offsets and placement kernels, with a
-// device-local copy of each tile into its stage rows standing in for the send / receive pair.
+// device, no communicator): a virtual group runs the same tiles, bands, offsets and placement kernels, with a
+// device-local copy of each tile into its frame rows (interleaved: its stage rows) standing in for the send /
+// receive pair.
 #include "multi.hpp"
 
 #include <hip/hip_runtime.h>
@@ -284,8 +288,9 @@ void group_destroy(rr_group* g) {
     trace("group_destroy %p: drained", (void*)g);
     for (ncclComm_t c : g->comms)
         if (c) (void)ncclCommDestroy(c);
-    // the parts' render contexts first: their last stream is the group's render stream of their set
-    // (rr_ctx::last_st), which rr_destroy synchronises and which must therefore still exist
+    // the parts' render contexts first, then the group's streams: a context waits only on its own event (rr_ctx::ev_out,
+    // recorded after each call's work) and never touches a stream after its call returns, but destroying the contexts
+    // while the streams still exist keeps the teardown order obviously safe (the round-4 hang)
     for (int b = 0; b < 2; ++b)
         for (size_t l = 0; l < g->subs[b].size(); ++l)
             if (g->subs[b][l]) {
