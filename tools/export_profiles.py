@@ -24,7 +24,7 @@ def export(tag, wl):
     shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(out_dir, f"{wl}_kernel_stats.csv"))
     # the frame's render kernels: the chain kernel (scenes with reflections: one launch per frame, bench.py's "chain")
     # or the fused trace+shade kernel per level ("trace_shade")
-    chain = [r for r in levels if r["kernel"].startswith("chain_kernel")]
+    chain = [r for r in levels if r["kernel"].startswith(("chain_kernel", "tree_kernel"))]
     shade = chain or [r for r in levels if r["kernel"].startswith("shade_kernel")]
     key = "chain" if chain else "trace_shade"
     n = len(shade)  # launches per frame (levels)
@@ -32,7 +32,8 @@ def export(tag, wl):
     hbm = [(2 * r["FETCH_SIZE"] + r["WRITE_SIZE"]) * 1024 for r in shade if "FETCH_SIZE" in r and "WRITE_SIZE" in r]
     busy_w = sum(r.get("valu_busy", 0) * r["mean_us"] for r in shade)
     summary = {
-        "workload": wl, "kernel": ("chain (chain_kernel: every reflection chain inside its camera wave, one launch)"
+        "workload": wl, "kernel": ("chain (chain_kernel / tree_kernel: every reflection chain or color_at tree inside its "
+                                   "camera wave, one launch)"
                                    if chain else "trace_shade (shade_kernel<..., FUSED, ...>, one launch per level)"),
         "launches_per_frame": n, "frame_kernel_us": round(tot_us, 2), "mean_launch_us": round(tot_us / n, 2),
         "hbm_bytes_per_launch": (sum(hbm) / len(hbm)) if len(hbm) == n else None,
