@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/final
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread \
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -rP -p no:cacheprovider --timeout 300 --timeout-method thread \
   > gpurun_out/final/gpu_tests.log 2>&1 || { tail -20 gpurun_out/final/gpu_tests.log; exit 1; }
 tail -1 gpurun_out/final/gpu_tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/final/smoke.log 2>&1 || exit 1
