@@ -81,7 +81,6 @@ struct rr_ctx {
         int64_t hs, lrows;
         int32_t aa, part, nparts, block_rows;
         int32_t pw, pad;
-        int32_t row0, pad2;
     } tile_key{};
     bool tiles_valid = false;
     // level-0 launch order of one-batch fused frames: every wave stores its tile's cost (clock cycles) and the
@@ -299,7 +298,6 @@ int tile_bundles(rr_ctx* c, const rr::LevelArgs& base_args, hipStream_t st, cons
     key.nparts = T.nparts;
     key.block_rows = T.block_rows;
     key.pw = T.pw;
-    key.row0 = T.row0;
     if (!c->tiles_valid || std::memcmp(&key, &c->tile_key, sizeof key) != 0) {
         if (T.pw)
             HIPCHK(rr::launch_pixel_wave_bundles(T, c->tiles.as<float>(), n_tiles, st));
@@ -438,7 +436,6 @@ int run_levels(rr_ctx* c, const rr::LevelArgs& base_args, int64_t total, int max
         key.nparts = T0.nparts;
         key.block_rows = T0.block_rows;
         key.pw = T0.pw;
-        key.row0 = T0.row0;
         key.pad = (chain ? 1 : 0) | (order_group == 1 ? 2 : 0);  // chain and level-0-only frames of one layout, and
                                                                   // each order unit, keep orders of their own
         if (c->order_tiles != n_tiles || std::memcmp(&key, &c->order_key, sizeof key) != 0) {
@@ -1001,10 +998,18 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     int rc = rr::render_validate(c, cam, o);
     if (rc != RR_OK) return rc;
     HIPCHK(hipSetDevice(c->device));
-    const int32_t block = o->block_rows > 0 ? o->block_rows : 8;
+    int32_t block = o->block_rows > 0 ? o->block_rows : 8;
     const int64_t H = cam->vsize / o->aa, W = cam->hsize / o->aa;
     const int64_t rows = opts_rows(o, H);
     const int64_t local_rows = rows * o->aa;
+    // a band [row_begin, row_end) is part row_begin / block of nparts = 1: the kernels' row arithmetic
+    // (bi * nparts + part) * block + kb is then row_begin + the local row, with a block that divides row_begin (8
+    // rows, else 2 — pixel waves need an even block — else 1)
+    int32_t part = o->part;
+    if (o->row_begin != 0 || o->row_end != 0) {
+        if (o->row_begin % block != 0) block = o->row_begin % 2 == 0 ? 2 : 1;
+        part = o->row_begin / block;
+    }
     const int64_t total = local_rows * cam->hsize;
     // Everything is enqueued on the caller's stream (no cross-stream events per call: a HIP event
     // handoff between streams costs host time every frame).  The context's workspace is reused, so
@@ -1034,10 +1039,9 @@ int rr_render_device(rr_ctx* c, const rr_camera* cam, const rr_render_opts* o, v
     A.hs = cam->hsize;
     A.lrows = local_rows;
     A.aa = o->aa;
-    A.part = o->part;
+    A.part = part;
     A.nparts = o->nparts;
     A.block_rows = block;
-    A.row0 = o->row_begin;  // 0 unless a band (check_opts)
     A.rays0 = nullptr;
     A.seed = o->seed;
     A.jitter_mode = o->jitter_mode;

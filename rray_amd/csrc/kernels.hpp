@@ -16,7 +16,6 @@ struct LevelArgs {
     int64_t hs;              // supersampled width
     int64_t lrows;           // part-local supersampled rows (level-0 camera rays run in 8x8 tiles)
     int32_t aa, part, nparts, block_rows;
-    int32_t row0;            // a band render (rr_render_opts row_begin / row_end): the band's first output row (else 0)
     uint32_t aa_magic, br_magic;  // floor(2^32 / d) for d = aa, block_rows (>= 2; 0 when d == 1)
     int32_t tile_fast;       // level-0 tiles all full 8x8 and the batch tile-aligned: wave = one tile
     uint32_t tiles_per_row;  // hs / 8 (tile_fast)
