@@ -70,7 +70,7 @@ struct rr_ctx {
     bool has_scene = false;
     rr::HostScene host;
     rr::DevScene S{};
-    DBuf culls, chunks, nodes, groups, shapes, tris, mats, pats, lights, textures, texels;
+    DBuf culls, inner, chunks, nodes, groups, shapes, tris, mats, pats, lights, textures, texels;
     // workspace
     DBuf counters, lcount, hit, n12, n1n2, ev_a, ev_b, canvas, rays0, qout;
     DBuf deep, deep_count;  // chain kernels' deep queue (rr::DeepRec segments) and its segment counters
@@ -776,7 +776,7 @@ void rr_destroy(rr_ctx* c) {
     rr::trace("rr_destroy %p: synchronise", (void*)c);
     if (c->stream) (void)sync_ctx(c);
     rr::trace("rr_destroy %p: free", (void*)c);
-    for (DBuf* b : {&c->culls, &c->chunks, &c->nodes, &c->groups, &c->shapes, &c->tris, &c->mats, &c->pats, &c->lights, &c->textures, &c->texels, &c->counters,
+    for (DBuf* b : {&c->culls, &c->inner, &c->chunks, &c->nodes, &c->groups, &c->shapes, &c->tris, &c->mats, &c->pats, &c->lights, &c->textures, &c->texels, &c->counters,
                     &c->lcount, &c->hit, &c->n12, &c->n1n2, &c->ev_a, &c->ev_b, &c->canvas, &c->rays0, &c->qout, &c->tiles,
                     &c->tile_cost, &c->tile_perm, &c->tile_hist, &c->deep, &c->deep_count})
         b->release();
@@ -809,6 +809,7 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     HIPCHK(sync_ctx(c));  // renders in flight may still read the previous scene
     hipStream_t st = c->stream;
     HIPCHK(upload(c->culls, hs.culls, st));
+    HIPCHK(upload(c->inner, hs.inner, st));
     HIPCHK(upload(c->chunks, hs.chunks, st));
     HIPCHK(upload(c->nodes, hs.nodes, st));
     HIPCHK(upload(c->groups, hs.groups, st));
@@ -828,6 +829,7 @@ int rr_scene_upload(rr_ctx* c, const rr_scene_desc* d) {
     c->tiles_valid = false;
     rr::DevScene& S = c->S;
     S.culls = c->culls.as<rr::DevCull>();
+    S.inner = c->inner.as<rr::DevCull>();
     S.chunks = c->chunks.as<rr::DevChunk>();
     S.n_chunks = (int32_t)c->host.chunks.size();
     S.n_free = 0;

@@ -297,6 +297,43 @@ static void mark_own_safe(HostScene& hs) {
     }
 }
 
+// Inner balls (render_levels.inc area_in_umbra): for a sphere outside any CSG, a ball that lies inside the set its exact
+// test reports — the unit sphere under the world-to-object transform A the walks apply (A_l x + A_t, every ancestor's
+// inverse and the node's): centre C = A^-1 (0, 0, 0) = the forward transform of the origin, radius 1 / sigma_max(A_l)
+// (|A_l (x - C)| <= sigma_max |x - C|), shrunk by 1e-6 relative and by the f32 rounding of the stored centre.  Other
+// nodes get radius 0 (none).
+static void mark_inner_balls(HostScene& hs) {
+    hs.inner.assign(hs.nodes.size(), DevCull{{0.0f, 0.0f, 0.0f}, 0.0f});
+    for (size_t ni = 0; ni < hs.nodes.size(); ++ni) {
+        const DevNode& nd = hs.nodes[ni];
+        if (nd.kind != RR_SPHERE || (nd.flags & NF_IN_CSG)) continue;
+        M4 inv = identity();
+        for (int a = (int)ni; a >= 0; a = hs.nodes[a].parent) {
+            M4 nfull = identity();
+            for (int e = 0; e < 12; ++e) nfull.m[e] = hs.nodes[a].inv[e];
+            inv = multiply(inv, nfull);  // the node's inverse first, the root's last
+        }
+        const M4 fwd = inverse(inv);
+        const Tup c = mul(fwd, point(0.0, 0.0, 0.0));
+        const double smax = sigma_max(inv);
+        // how far the computed centre is from the object-space origin (the inverse's rounding): shrinks the ball
+        const Tup oc = mul(inv, c);
+        const double res = std::sqrt(oc.x * oc.x + oc.y * oc.y + oc.z * oc.z);
+        if (!std::isfinite(c.x) || !std::isfinite(c.y) || !std::isfinite(c.z) || !(smax > 0.0) || !std::isfinite(smax) ||
+            !(res < 0.5))
+            continue;
+        const float cf[3] = {(float)c.x, (float)c.y, (float)c.z};
+        const double shift = std::sqrt(((double)cf[0] - c.x) * ((double)cf[0] - c.x) + ((double)cf[1] - c.y) * ((double)cf[1] - c.y) +
+                                       ((double)cf[2] - c.z) * ((double)cf[2] - c.z));
+        const double scale = std::fabs(c.x) + std::fabs(c.y) + std::fabs(c.z);
+        const double r = ((1.0 - res) / smax) * (1.0 - 1e-6) - 2.0 * shift - 1e-9 * (scale + 1.0 / smax);
+        if (!(r > 0.0)) continue;
+        DevCull& b = hs.inner[ni];
+        for (int k = 0; k < 3; ++k) b.c[k] = cf[k];
+        b.r = std::nextafter((float)r, 0.0f);  // rounded down
+    }
+}
+
 void build_chunks(HostScene& hs) {
     hs.chunks.clear();
     const int N = (int)hs.nodes.size();
@@ -809,6 +846,7 @@ int flatten_scene(const rr_scene_desc& d, HostScene& out, std::string& err) {
     }
     out.tri_inline = n_tri > 0 && n_inline == n_tri ? 1 : 0;
     mark_own_safe(out);
+    mark_inner_balls(out);
     for (DevChunk& ch : out.chunks) {  // runs of one kind (DevChunk.run)
         ch.run = CR_NONE;
         const DevNode& a = out.nodes[ch.start];

@@ -11,6 +11,7 @@ namespace rr {
 struct HostScene {
     std::vector<DevNode> nodes;
     std::vector<DevCull> culls;  // one per node
+    std::vector<DevCull> inner;  // one per node: a ball inside the set the node's exact test reports (r 0: none)
     std::vector<DevChunk> chunks;
     std::vector<DevGroup> groups;
     std::vector<DevTri> tris;

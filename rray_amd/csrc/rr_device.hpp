@@ -135,6 +135,7 @@ struct alignas(16) DevChunk {
 
 struct DevScene {
     const DevCull* culls;
+    const DevCull* inner;     // per node: a ball inside what its exact test reports (spheres; r == 0: none)
     const DevChunk* chunks;
     const DevNode* nodes;
     const DevGroup* groups;
